@@ -1,0 +1,178 @@
+/*
+ * nqk.h — C ABI of libnqk.so, the MI355X (gfx950) backend for numpy-quant's
+ * quantized per-node execution hot path.
+ *
+ * The reference has no FFI of its own: its operator boundary is
+ *   onnx_operator_implementation(op, inputs, attrs)   numpy_quant/model.py:65-213
+ * plus the L1 array functions in numpy_quant/numpy_quantization.py:7-72 and
+ * numpy_quant/numpy_helper.py:73-112.  Each entry point below replaces one of
+ * those (cited per function); the Python host (numpy-quant_amd/numpy_quant/_lib.py)
+ * binds them with ctypes exactly as INTEGRATION.md shows.
+ *
+ * Conventions
+ *   - plain pointers and sizes only; device pointers come from nqk_malloc;
+ *   - every call is asynchronous on the library's single stream for the current
+ *     device (one process per GPU), except the *_sync / memcpy_d2h calls;
+ *   - kernels never allocate; callers own every buffer;
+ *   - return 0 on success, <0 on error; nqk_last_error() describes the last error
+ *     of the calling thread (the Python layer raises ValueError / RuntimeError);
+ *   - dtype codes (NQK_*) select the storage of integer tensors:
+ *       quantized values of bit width bw live in the narrowest of i8/i16/i32/i64
+ *       that holds [-2^(bw-1), 2^(bw-1)-1] (the reference stores int64 always,
+ *       tensor.py:158-166; values are identical, storage is narrower).
+ *   - "zero point term" of a MatMul output (numpy_quantization.py:49-61) is never
+ *     materialised: it is rebuilt on the fly from per-row sums of A and per-column
+ *     sums of B:  zpt[b,m,n] = row[a(b),m]*zpb + col[b(b),n]*zpa - zpa*zpb*K,
+ *     with the terms enabled by NQK_ZP_ROW / NQK_ZP_COL / NQK_ZP_SCALAR flags.
+ *   - batch map (broadcast batch dims of np.matmul, numpy_quantization.py:47): the
+ *     output batch index b is split as (bo, bi) = (b / inner, b % inner) and the
+ *     A / B matrix index is bo*ao + bi*ai / bo*bo_ + bi*bi_ (in matrices); `bmap`
+ *     is a HOST array of 5 int64 (NULL = no broadcast: every operand has `batch`).
+ */
+#ifndef NQK_H
+#define NQK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum nqk_dtype { NQK_I8 = 1, NQK_I16 = 2, NQK_I32 = 3, NQK_I64 = 4, NQK_F32 = 5 };
+
+enum nqk_zp_flags {
+  NQK_ZP_NONE = 0,
+  NQK_ZP_SCALAR = 1,  /* subtract a scalar zero point zp                       */
+  NQK_ZP_ROW = 2,     /* + row[a(b), m] * zpb  (rowsum(A) term, zero_point_b)   */
+  NQK_ZP_COL = 4,     /* + col[b(b), n] * zpa  (colsum(B) term, zero_point_a)   */
+  NQK_ZP_KCONST = 8,  /* - zpa * zpb * K       (both operands asymmetric)       */
+  NQK_ZP_FULL = 16    /* + row[i]: a materialised int64 zero-point array (flat) */
+};
+
+/* ---------------------------------------------------------------- runtime */
+int nqk_init(int device);              /* select device, create the stream (idempotent) */
+int nqk_device_count(int* count);
+const char* nqk_last_error(void);
+int nqk_malloc(void** ptr, size_t bytes);
+int nqk_free(void* ptr);
+int nqk_memcpy_h2d(void* dst, const void* src, size_t bytes);   /* returns when the copy is done */
+int nqk_memcpy_d2h(void* dst, const void* src, size_t bytes);   /* stream-ordered, synchronous */
+int nqk_memcpy_d2d(void* dst, const void* src, size_t bytes);   /* async */
+int nqk_memset(void* ptr, int value, size_t bytes);             /* async */
+int nqk_sync(void);
+int nqk_stream(void** stream);         /* the library's hipStream_t */
+/* stream timers: record start / stop events, nqk_timer_ms waits for stop */
+int nqk_timer_start(void);
+int nqk_timer_stop(void);
+int nqk_timer_ms(float* ms);
+/* hipGraph capture of everything issued between begin and end */
+int nqk_graph_begin(void);
+int nqk_graph_end(void** graph_exec);
+int nqk_graph_launch(void* graph_exec);
+int nqk_graph_destroy(void* graph_exec);
+
+/* ------------------------------------------------- L1: quantization kernels */
+/* quantize  numpy_quantization.py:24-34 (tensor.py:299-301 quantize_tensor)
+ *   q = int(rint(clip(f64(zp) + f64(f32(x / s)), lo, hi)))   (has_zp)
+ *   q = int(rint(clip(f32(x / s), f32(lo), f32(hi))))        (!has_zp)
+ * optional rowsum (int64, per row of length row_len, may be NULL). */
+int nqk_quantize(const float* x, void* q, int q_dtype, int64_t n, float scale,
+                 int64_t zp, int has_zp, int bit_width, int64_t* rowsum, int64_t row_len);
+
+/* dequantize  numpy_quantization.py:37-41, tensor.py:261-265
+ *   out = f32( f64(q - zpt) * f64(s) ) over out[batch][M][N]; zpt from zp_flags.
+ *   For a plain tensor pass batch=1, M=1, N=n and NQK_ZP_SCALAR or NONE. */
+int nqk_dequantize(const void* q, int q_dtype, float* out, int64_t batch, int64_t M, int64_t N,
+                   float scale, int zp_flags, int64_t zp, int64_t zpa, int64_t zpb, int64_t K,
+                   const int64_t* row, const int64_t* col, const int64_t* bmap /* 5 */);
+
+/* requantize  numpy_quantization.py:64-72 (+ QTensor.__add__ of the Gemm bias,
+ * tensor.py:255-259, model.py:130):  d = dequantize(acc + bias[n]);
+ *   q = int(clip(rint(f64(rz) + f64(f32(f32(1/rs) * d))), lo, hi)) */
+int nqk_requantize(const void* acc, int acc_dtype, const void* bias, int bias_dtype,
+                   void* out, int out_dtype, int64_t batch, int64_t M, int64_t N, float scale,
+                   int zp_flags, int64_t zp, int64_t zpa, int64_t zpb, int64_t K,
+                   const int64_t* row, const int64_t* col, const int64_t* bmap,
+                   float res_scale, int64_t res_zp, int has_res_zp, int bit_width);
+
+/* row / column sums of an integer matrix batch (the q_matmul zero-point terms,
+ * numpy_quantization.py:52,55,58-59), int64: row[b][m] = sum_k A[b][m][k] (row-major,
+ * lda), col[b][n] = sum_k B[b][k][n] (B given TRANSPOSED as Bt[b][n][k], ldb). */
+int nqk_rowsum(const void* a, int dtype, int64_t* out, int64_t batch, int64_t rows, int64_t k,
+               int64_t ld, int64_t batch_stride);
+
+/* ------------------------------------------------------ L1: q_matmul GEMMs */
+/* q_matmul's integer product, numpy_quantization.py:47:
+ *   C[b][m][n] = sum_k A[b'][m][k] * Bt[b''][n][k]     (int32 out)
+ * int8 operands on v_mfma_i32_32x32x32_i8; lda/ldb multiples of 16 bytes; K is
+ * zero-padded by the caller to a multiple of 16 (zeros add nothing). */
+int nqk_qgemm_i8(const int8_t* a, const int8_t* bt, int32_t* c, int64_t batch, int64_t M,
+                 int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc,
+                 const int64_t* bmap /* 5: inner, ao, ai, bo, bi in matrices */,
+                 int64_t a_mat_stride, int64_t b_mat_stride, int64_t c_mat_stride);
+/* any-width integer operands (bit widths > 8, tiny shapes), int64 accumulation on
+ * VALU; B[K][N] addressed by element strides (b_sk, b_sn) */
+int nqk_qgemm_generic(const void* a, int a_dtype, const void* b, int b_dtype, int64_t* c,
+                      int64_t batch, int64_t M, int64_t N, int64_t K, int64_t a_sm, int64_t a_sk,
+                      int64_t b_sk, int64_t b_sn, int64_t ldc, const int64_t* bmap,
+                      int64_t a_mat_stride, int64_t b_mat_stride, int64_t c_mat_stride);
+
+/* ------------------------------------------- float32 GEMM (BLAS-order exact) */
+/* C = A[M][K] . B[K][N] (element strides a_sm/a_sk, b_sk/b_sn).  Every output element is the
+ * reference BLAS's summation: K is cut into OpenBLAS level-3 blocks (GEMM_Q=384
+ * rule), each block a k-ordered fmaf chain from 0, blocks added in order.  Used
+ * by Conv (numpy_helper.py:73-92 x.dot(w)) and by float MatMul/Gemm of the
+ * calibration forward (model.py:153-157, 122-131 via np.matmul). */
+int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch, int64_t M, int64_t N,
+              int64_t K, int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc,
+              const int64_t* bmap, int64_t a_mat_stride, int64_t b_mat_stride, int64_t c_mat_stride);
+
+/* im2col for Conv (numpy_helper.py:18-70): x NCHW f32 -> cols[N*Ho*Wo][KH*KW*C]
+ * (column order kh, kw, c), zero padding pads = (ph0, pw0, ph1, pw1). */
+int nqk_im2col(const float* x, float* cols, int64_t n, int64_t c, int64_t h, int64_t w,
+               int64_t kh, int64_t kw, int64_t ph0, int64_t pw0, int64_t sh, int64_t sw,
+               int64_t ho, int64_t wo);
+
+/* ------------------------------------------- float ops (model.py:65-213) */
+enum nqk_binop { NQK_ADD = 0, NQK_SUB = 1, NQK_MUL = 2, NQK_DIV = 3 };
+/* out[i] = a[ia] op b[ib] over an N-d broadcast (ndim <= 6; strides in elements) */
+int nqk_binary_f32(int op, const float* a, const float* b, float* out, int ndim,
+                   const int64_t* shape, const int64_t* a_strides, const int64_t* b_strides);
+enum nqk_unop { NQK_NEG = 0, NQK_EXP = 1, NQK_ERF = 2, NQK_SQRT = 3, NQK_RELU = 4,
+                NQK_SIGMOID = 5, NQK_RECIP = 6, NQK_TANH = 7 };
+/* NumPy-exact where it matters: EXP is numpy's AVX512F float32 exp algorithm
+ * (bit-identical to np.exp on all 2^32 inputs), ERF is numpy_helper.py:95-112. */
+int nqk_unary_f32(int op, const float* x, float* out, int64_t n);
+/* x + scalar (FTensor.__add__ with a Python float, tensor.py:158-164) */
+int nqk_add_scalar_f32(const float* x, float s, float* out, int64_t n);
+/* Softmax over the last axis (tensor.py:211-218): e = exp(x - max); e / pairwise_sum(e) */
+int nqk_softmax_lastdim(const float* x, float* out, int64_t rows, int64_t cols);
+/* LayerNormalization over the last axis (model.py:134-152), NumPy pairwise means */
+int nqk_layernorm_lastdim(const float* x, const float* gamma, const float* beta, float* out,
+                          int64_t rows, int64_t cols, float eps);
+/* mean over the last axis with NumPy's pairwise summation (np.mean f32) */
+int nqk_mean_lastdim(const float* x, float* out, int64_t rows, int64_t cols);
+/* global min and max (calibration, model.py:333-336) -> out[0]=min, out[1]=max */
+int nqk_minmax_f32(const float* x, int64_t n, float* out2, float* scratch, int64_t scratch_len);
+/* N-d strided copy for Transpose / Concat / Slice / Expand / Gather / padding
+ * (element size 1, 2, 4 or 8 bytes; ndim <= 6; strides in elements) */
+int nqk_copy_strided(const void* src, void* dst, int elem_size, int ndim, const int64_t* shape,
+                     const int64_t* src_strides, const int64_t* dst_strides);
+/* where(cond, a, b) with broadcasting (tensor.py:323-325), f32 */
+int nqk_where_f32(const int64_t* cond, const float* a, const float* b, float* out, int ndim,
+                  const int64_t* shape, const int64_t* c_strides, const int64_t* a_strides,
+                  const int64_t* b_strides);
+
+/* ------------------------------------------------ multi-GPU replicas (RCCL) */
+int nqk_comm_unique_id(void* id128);                         /* rank 0 */
+int nqk_comm_init(const void* id128, int nranks, int rank);
+int nqk_comm_bcast(void* buf, size_t bytes, int root);
+int nqk_comm_gather(const void* send, void* recv, size_t bytes_per_rank, int root);
+int nqk_comm_barrier(void);
+int nqk_comm_destroy(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NQK_H */

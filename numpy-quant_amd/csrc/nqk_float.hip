@@ -1,0 +1,460 @@
+// Float32 operators of the QModel node loop (numpy_quant/model.py:65-213,
+// tensor.py:119-225) — the "else" branch of QModel.__call__ (model.py:528-538)
+// runs these on dequantized inputs.  They are written to be NumPy-exact:
+//   * elementwise f32 +,-,*,/ and sqrt are IEEE correctly rounded, no contraction
+//     (-ffp-contract=off) — the same as NumPy's SIMD loops;
+//   * exp is NumPy's AVX512F float32 algorithm (Cody-Waite reduction, 5/2 rational
+//     minimax, scalef), bit-identical to np.exp on every one of the 2^32 inputs
+//     (checked exhaustively on the host, tests/test_numerics.py on the GPU);
+//   * sums / means over the last axis follow NumPy's pairwise summation
+//     (blocks of <= 128 with 8 interleaved accumulators, recursive halving at
+//     multiples of 8), so LayerNormalization and Softmax match bit for bit.
+#include "nqk_common.h"
+
+namespace nqk {
+namespace {
+
+// ------------------------------------------------------------------ numpy float32 exp
+__device__ __forceinline__ float np_expf(float x) {
+  const float xmax = 88.72283935546875f, xmin = -103.97208404541015625f;
+  if (x != x) return x;
+  const bool over = x >= xmax, under = x <= xmin;
+  float xx = (over || under) ? 0.0f : x;
+  float q = xx * 1.442695040888963407359924681001892137f;
+  q = q + 0x1.800000p+23f;
+  q = q - 0x1.800000p+23f;
+  float r = __builtin_fmaf(q, -6.93145752e-1f, xx);
+  r = __builtin_fmaf(q, -1.42860677e-6f, r);
+  r = __builtin_fmaf(q, 0.0f, r);
+  float num = __builtin_fmaf(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);
+  num = __builtin_fmaf(num, r, 5.114512081637298353406e-02f);
+  num = __builtin_fmaf(num, r, 2.473615434895520810817e-01f);
+  num = __builtin_fmaf(num, r, 7.257664613233124478488e-01f);
+  num = __builtin_fmaf(num, r, 9.999999999980870924916e-01f);
+  float den = __builtin_fmaf(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
+  den = __builtin_fmaf(den, r, 1.0f);
+  float poly = num / den;
+  poly = __builtin_ldexpf(poly, (int)q);
+  if (over) poly = __builtin_inff();
+  if (under) poly = 0.0f;
+  return poly;
+}
+
+// numpy_helper.py:95-112 (A&S 7.1.26), float32 throughout
+__device__ __forceinline__ float ref_erf(float x) {
+  float sgn = (x > 0.0f) ? 1.0f : ((x < 0.0f) ? -1.0f : (x == 0.0f ? 0.0f : x));
+  float ax = __builtin_fabsf(x);
+  float t = 1.0f / (1.0f + 0.3275911f * ax);
+  float p = 1.061405429f * t + -1.453152027f;
+  p = p * t;
+  p = p + 1.421413741f;
+  p = p * t + -0.284496736f;
+  p = p * t + 0.254829592f;
+  float y = 1.0f - p * t * np_expf(-ax * ax);
+  return sgn * y;
+}
+
+template <int OP>
+__device__ __forceinline__ float unary(float x) {
+  if constexpr (OP == NQK_NEG) return -x;
+  else if constexpr (OP == NQK_EXP) return np_expf(x);
+  else if constexpr (OP == NQK_ERF) return ref_erf(x);
+  else if constexpr (OP == NQK_SQRT) return __builtin_sqrtf(x);
+  else if constexpr (OP == NQK_RELU) return (x > 0.0f ? 1.0f : 0.0f) * x;   // (x > 0) * x
+  else if constexpr (OP == NQK_SIGMOID) return 1.0f / (np_expf(-x) + 1.0f);  // tensor.py:205-206
+  else if constexpr (OP == NQK_RECIP) return 1.0f / x;
+  else return tanhf(x);
+}
+
+template <int OP>
+__global__ void k_unary(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = unary<OP>(x[i]);
+}
+
+__global__ void k_add_scalar(const float* __restrict__ x, float s, float* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = x[i] + s;
+}
+
+struct Nd {
+  int ndim;
+  int64_t shape[6];
+  int64_t s0[6], s1[6], s2[6];
+};
+
+__device__ __forceinline__ void nd_offsets(const Nd& d, int64_t i, int64_t& o0, int64_t& o1, int64_t& o2) {
+  o0 = o1 = o2 = 0;
+  for (int k = d.ndim - 1; k >= 0; --k) {
+    int64_t c = i % d.shape[k];
+    i /= d.shape[k];
+    o0 += c * d.s0[k];
+    o1 += c * d.s1[k];
+    o2 += c * d.s2[k];
+  }
+}
+
+template <int OP>
+__global__ void k_binary(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ out,
+                         int64_t total, Nd d) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    int64_t oa, ob, unused;
+    nd_offsets(d, i, oa, ob, unused);
+    float x = a[oa], y = b[ob], r;
+    if constexpr (OP == NQK_ADD) r = x + y;
+    else if constexpr (OP == NQK_SUB) r = x - y;
+    else if constexpr (OP == NQK_MUL) r = x * y;
+    else r = x / y;
+    out[i] = r;
+  }
+}
+
+__global__ void k_where(const int64_t* __restrict__ c, const float* __restrict__ a, const float* __restrict__ b,
+                        float* __restrict__ out, int64_t total, Nd d, Nd d2) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    int64_t oc, oa, ob, u;
+    nd_offsets(d, i, oc, oa, ob);
+    (void)u;
+    out[i] = c[oc] ? a[oa] : b[ob];
+  }
+}
+
+template <typename T>
+__global__ void k_copy_nd(const T* __restrict__ src, T* __restrict__ dst, int64_t total, Nd d) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    int64_t os, od, u;
+    nd_offsets(d, i, os, od, u);
+    dst[od] = src[os];
+  }
+}
+
+// ------------------------------------------------------------------ NumPy pairwise sum
+// The recursion of NumPy's pairwise_sum (n < 8: sequential; n <= 128: 8 interleaved
+// accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the n % 8 tail;
+// else split at n/2 rounded down to a multiple of 8) depends only on n, so the host
+// flattens it into leaves + a post-order combine program shared by every row.
+constexpr int kMaxLeaves = 64;
+struct PwPlan {
+  int nleaf, nops;
+  int start[kMaxLeaves], len[kMaxLeaves];
+  signed char ops[2 * kMaxLeaves];  // >= 0: push leaf; -1: pop b, pop a, push a + b
+};
+
+static int build_plan(int64_t n, int64_t s, PwPlan& p) {
+  if (n <= 128) {
+    if (p.nleaf >= kMaxLeaves) return -1;
+    p.start[p.nleaf] = (int)s;
+    p.len[p.nleaf] = (int)n;
+    p.ops[p.nops++] = (signed char)p.nleaf++;
+    return 0;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  if (build_plan(n2, s, p) || build_plan(n - n2, s + n2, p)) return -1;
+  p.ops[p.nops++] = -1;
+  return 0;
+}
+
+// one 64-lane block per row; `v` is the row in LDS, scratch holds 8 partials per leaf
+__device__ float row_pairwise_sum(const float* v, const PwPlan& p, float* part, float* leafv) {
+  const int lane = threadIdx.x;
+  for (int c = lane; c < p.nleaf * 8; c += 64) {
+    int l = c >> 3, j = c & 7;
+    int L = p.len[l], s = p.start[l];
+    float r = 0.0f;
+    if (L >= 8) {
+      r = v[s + j];
+      int end = L - (L % 8);
+      for (int i = 8 + j; i < end; i += 8) r = r + v[s + i];
+    }
+    part[c] = r;
+  }
+  __syncthreads();
+  for (int l = lane; l < p.nleaf; l += 64) {
+    int L = p.len[l], s = p.start[l];
+    float res;
+    if (L < 8) {
+      res = 0.0f;
+      for (int i = 0; i < L; ++i) res = res + v[s + i];
+    } else {
+      const float* r = part + l * 8;
+      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      for (int i = L - (L % 8); i < L; ++i) res = res + v[s + i];
+    }
+    leafv[l] = res;
+  }
+  __syncthreads();
+  float* total = leafv + kMaxLeaves;
+  if (lane == 0) {
+    float st[16];
+    int sp = 0;
+    for (int o = 0; o < p.nops; ++o) {
+      int op = p.ops[o];
+      if (op >= 0) st[sp++] = leafv[op];
+      else { float b = st[--sp]; float a = st[--sp]; st[sp++] = a + b; }
+    }
+    *total = st[0];
+  }
+  __syncthreads();
+  float t = *total;
+  __syncthreads();
+  return t;
+}
+
+__global__ void __launch_bounds__(64)
+k_softmax(const float* __restrict__ x, float* __restrict__ out, int64_t rows, int64_t cols, PwPlan p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* v = sm;
+  float* part = sm + cols;
+  float* leafv = part + kMaxLeaves * 8;
+  const int lane = threadIdx.x;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const float* xr = x + r * cols;
+    float mx = -__builtin_inff();
+    for (int64_t i = lane; i < cols; i += 64) {
+      float t = xr[i];
+      v[i] = t;
+      mx = t > mx ? t : mx;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      float o = __shfl_xor(mx, off, 64);
+      mx = o > mx ? o : mx;
+    }
+    const float nm = -mx;
+    for (int64_t i = lane; i < cols; i += 64) v[i] = np_expf(v[i] + nm);
+    __syncthreads();
+    float s = row_pairwise_sum(v, p, part, leafv);
+    float* orow = out + r * cols;
+    for (int64_t i = lane; i < cols; i += 64) orow[i] = v[i] / s;
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(64)
+k_layernorm(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
+            float* __restrict__ out, int64_t rows, int64_t cols, float eps, PwPlan p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* v = sm;
+  float* part = sm + cols;
+  float* leafv = part + kMaxLeaves * 8;
+  const int lane = threadIdx.x;
+  const float fcols = (float)cols;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const float* xr = x + r * cols;
+    for (int64_t i = lane; i < cols; i += 64) v[i] = xr[i];
+    __syncthreads();
+    const float mean = row_pairwise_sum(v, p, part, leafv) / fcols;
+    const float nmean = -mean;
+    for (int64_t i = lane; i < cols; i += 64) {
+      float d = v[i] + nmean;
+      v[i] = d * d;
+    }
+    __syncthreads();
+    const float var = row_pairwise_sum(v, p, part, leafv) / fcols;
+    const float inv = 1.0f / __builtin_sqrtf(var + eps);
+    float* orow = out + r * cols;
+    for (int64_t i = lane; i < cols; i += 64) {
+      float d = xr[i] + nmean;
+      orow[i] = ((d * inv) * g[i]) + b[i];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(64)
+k_mean_rows(const float* __restrict__ x, float* __restrict__ out, int64_t rows, int64_t cols, PwPlan p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* v = sm;
+  float* part = sm + cols;
+  float* leafv = part + kMaxLeaves * 8;
+  const int lane = threadIdx.x;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    for (int64_t i = lane; i < cols; i += 64) v[i] = x[r * cols + i];
+    __syncthreads();
+    float s = row_pairwise_sum(v, p, part, leafv);
+    if (lane == 0) out[r] = s / (float)cols;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ min / max (calibration)
+__global__ void k_minmax_partial(const float* __restrict__ x, int64_t n, float* __restrict__ part) {
+  float mn = __builtin_inff(), mx = -__builtin_inff();
+  bool nan = false;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float t = x[i];
+    nan |= (t != t);
+    mn = t < mn ? t : mn;
+    mx = t > mx ? t : mx;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    float a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  unsigned long long anynan = __ballot(nan);
+  __shared__ float smn[4], smx[4];
+  __shared__ int snan[4];
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[w] = mn; smx[w] = mx; snan[w] = anynan != 0; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int nw = blockDim.x >> 6;
+    bool nn = false;
+    for (int i = 0; i < nw; ++i) { mn = smn[i] < mn ? smn[i] : mn; mx = smx[i] > mx ? smx[i] : mx; nn |= snan[i] != 0; }
+    if (nn) { mn = __builtin_nanf(""); mx = mn; }
+    part[2 * blockIdx.x] = mn;
+    part[2 * blockIdx.x + 1] = mx;
+  }
+}
+
+__global__ void k_minmax_final(const float* __restrict__ part, int nparts, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  float mn = __builtin_inff(), mx = -__builtin_inff();
+  bool nan = false;
+  for (int i = 0; i < nparts; ++i) {
+    float a = part[2 * i], b = part[2 * i + 1];
+    nan |= (a != a) || (b != b);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (nan) { mn = __builtin_nanf(""); mx = mn; }
+  out[0] = mn;
+  out[1] = mx;
+}
+
+Nd make_nd(int ndim, const int64_t* shape, const int64_t* s0, const int64_t* s1, const int64_t* s2) {
+  Nd d{};
+  d.ndim = ndim;
+  for (int k = 0; k < ndim; ++k) {
+    d.shape[k] = shape[k];
+    d.s0[k] = s0 ? s0[k] : 0;
+    d.s1[k] = s1 ? s1[k] : 0;
+    d.s2[k] = s2 ? s2[k] : 0;
+  }
+  return d;
+}
+
+int64_t nd_total(int ndim, const int64_t* shape) {
+  int64_t t = 1;
+  for (int k = 0; k < ndim; ++k) t *= shape[k];
+  return t;
+}
+
+int row_plan(int64_t cols, PwPlan& p) {
+  p.nleaf = 0;
+  p.nops = 0;
+  if (cols <= 0 || build_plan(cols, 0, p)) return fail("row length not supported by the pairwise-sum plan (max 8192)");
+  return 0;
+}
+
+}  // namespace
+}  // namespace nqk
+
+using namespace nqk;
+
+extern "C" int nqk_binary_f32(int op, const float* a, const float* b, float* out, int ndim, const int64_t* shape,
+                              const int64_t* a_strides, const int64_t* b_strides) {
+  if (ndim < 0 || ndim > 6) return fail("nqk_binary_f32: ndim > 6");
+  int64_t total = nd_total(ndim, shape);
+  if (total <= 0) return 0;
+  Nd d = make_nd(ndim, shape, a_strides, b_strides, nullptr);
+  unsigned g = grid_for(total);
+  switch (op) {
+    case NQK_ADD: hipLaunchKernelGGL(k_binary<NQK_ADD>, dim3(g), dim3(kThreads), 0, stream(), a, b, out, total, d); break;
+    case NQK_SUB: hipLaunchKernelGGL(k_binary<NQK_SUB>, dim3(g), dim3(kThreads), 0, stream(), a, b, out, total, d); break;
+    case NQK_MUL: hipLaunchKernelGGL(k_binary<NQK_MUL>, dim3(g), dim3(kThreads), 0, stream(), a, b, out, total, d); break;
+    case NQK_DIV: hipLaunchKernelGGL(k_binary<NQK_DIV>, dim3(g), dim3(kThreads), 0, stream(), a, b, out, total, d); break;
+    default: return fail("nqk_binary_f32: bad op");
+  }
+  return launch_status("nqk_binary_f32");
+}
+
+extern "C" int nqk_unary_f32(int op, const float* x, float* out, int64_t n) {
+  if (n <= 0) return 0;
+  unsigned g = grid_for(n);
+  switch (op) {
+#define U(OPC) case OPC: hipLaunchKernelGGL(k_unary<OPC>, dim3(g), dim3(kThreads), 0, stream(), x, out, n); break;
+    U(NQK_NEG) U(NQK_EXP) U(NQK_ERF) U(NQK_SQRT) U(NQK_RELU) U(NQK_SIGMOID) U(NQK_RECIP) U(NQK_TANH)
+#undef U
+    default: return fail("nqk_unary_f32: bad op");
+  }
+  return launch_status("nqk_unary_f32");
+}
+
+extern "C" int nqk_add_scalar_f32(const float* x, float s, float* out, int64_t n) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_add_scalar, dim3(grid_for(n)), dim3(kThreads), 0, stream(), x, s, out, n);
+  return launch_status("nqk_add_scalar_f32");
+}
+
+static size_t row_smem(int64_t cols) { return (size_t)(cols + kMaxLeaves * 8 + kMaxLeaves + 4) * sizeof(float); }
+static unsigned row_grid(int64_t rows) { return (unsigned)(rows < 65536 * 4 ? rows : 65536 * 4); }
+
+extern "C" int nqk_softmax_lastdim(const float* x, float* out, int64_t rows, int64_t cols) {
+  if (rows <= 0) return 0;
+  PwPlan p;
+  if (row_plan(cols, p)) return -1;
+  hipLaunchKernelGGL(k_softmax, dim3(row_grid(rows)), dim3(64), row_smem(cols), stream(), x, out, rows, cols, p);
+  return launch_status("nqk_softmax_lastdim");
+}
+
+extern "C" int nqk_layernorm_lastdim(const float* x, const float* gamma, const float* beta, float* out, int64_t rows,
+                                     int64_t cols, float eps) {
+  if (rows <= 0) return 0;
+  PwPlan p;
+  if (row_plan(cols, p)) return -1;
+  hipLaunchKernelGGL(k_layernorm, dim3(row_grid(rows)), dim3(64), row_smem(cols), stream(), x, gamma, beta, out,
+                     rows, cols, eps, p);
+  return launch_status("nqk_layernorm_lastdim");
+}
+
+extern "C" int nqk_mean_lastdim(const float* x, float* out, int64_t rows, int64_t cols) {
+  if (rows <= 0) return 0;
+  PwPlan p;
+  if (row_plan(cols, p)) return -1;
+  hipLaunchKernelGGL(k_mean_rows, dim3(row_grid(rows)), dim3(64), row_smem(cols), stream(), x, out, rows, cols, p);
+  return launch_status("nqk_mean_lastdim");
+}
+
+extern "C" int nqk_minmax_f32(const float* x, int64_t n, float* out2, float* scratch, int64_t scratch_len) {
+  if (n <= 0) return fail("nqk_minmax_f32: empty tensor");
+  int64_t parts = scratch_len / 2;
+  if (parts < 1) return fail("nqk_minmax_f32: scratch too small");
+  unsigned g = grid_for(n, 256, parts < 2048 ? parts : 2048);
+  hipLaunchKernelGGL(k_minmax_partial, dim3(g), dim3(256), 0, stream(), x, n, scratch);
+  hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(64), 0, stream(), scratch, (int)g, out2);
+  return launch_status("nqk_minmax_f32");
+}
+
+extern "C" int nqk_copy_strided(const void* src, void* dst, int elem_size, int ndim, const int64_t* shape,
+                                const int64_t* src_strides, const int64_t* dst_strides) {
+  if (ndim < 0 || ndim > 6) return fail("nqk_copy_strided: ndim > 6");
+  int64_t total = nd_total(ndim, shape);
+  if (total <= 0) return 0;
+  Nd d = make_nd(ndim, shape, src_strides, dst_strides, nullptr);
+  unsigned g = grid_for(total);
+  switch (elem_size) {
+    case 1: hipLaunchKernelGGL(k_copy_nd<int8_t>, dim3(g), dim3(kThreads), 0, stream(), (const int8_t*)src, (int8_t*)dst, total, d); break;
+    case 2: hipLaunchKernelGGL(k_copy_nd<int16_t>, dim3(g), dim3(kThreads), 0, stream(), (const int16_t*)src, (int16_t*)dst, total, d); break;
+    case 4: hipLaunchKernelGGL(k_copy_nd<int32_t>, dim3(g), dim3(kThreads), 0, stream(), (const int32_t*)src, (int32_t*)dst, total, d); break;
+    case 8: hipLaunchKernelGGL(k_copy_nd<int64_t>, dim3(g), dim3(kThreads), 0, stream(), (const int64_t*)src, (int64_t*)dst, total, d); break;
+    default: return fail("nqk_copy_strided: element size must be 1, 2, 4 or 8");
+  }
+  return launch_status("nqk_copy_strided");
+}
+
+extern "C" int nqk_where_f32(const int64_t* cond, const float* a, const float* b, float* out, int ndim,
+                             const int64_t* shape, const int64_t* c_strides, const int64_t* a_strides,
+                             const int64_t* b_strides) {
+  if (ndim < 0 || ndim > 6) return fail("nqk_where_f32: ndim > 6");
+  int64_t total = nd_total(ndim, shape);
+  if (total <= 0) return 0;
+  Nd d = make_nd(ndim, shape, c_strides, a_strides, b_strides);
+  hipLaunchKernelGGL(k_where, dim3(grid_for(total)), dim3(kThreads), 0, stream(), cond, a, b, out, total, d, d);
+  return launch_status("nqk_where_f32");
+}

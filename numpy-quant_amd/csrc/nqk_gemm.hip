@@ -1,0 +1,313 @@
+// GEMMs of the hot path.
+//
+//  * nqk_qgemm_i8     — q_matmul's integer product (numpy_quantization.py:47) for
+//                       bit widths <= 8 on v_mfma_i32_32x32x32_i8.  int32
+//                       accumulation is exact: |a|,|b| <= 128, K < 2^17.
+//  * nqk_qgemm_generic — the same product for any storage width, int64 on VALU
+//                       (bit widths 9..32, tiny shapes such as the MLP).
+//  * nqk_sgemm        — float32 GEMM that reproduces the reference BLAS bit for
+//                       bit: OpenBLAS (scipy-openblas 0.3.29, SkylakeX kernels, the
+//                       one NumPy 2.2.6 ships on both hosts) cuts K into level-3
+//                       blocks (GEMM_Q = 384; a remainder in (Q, 2Q) is halved),
+//                       each block a k-ordered fmaf chain from 0, blocks summed in
+//                       order.  Verified against np.dot for K <= 768.
+//  * nqk_im2col       — numpy_helper.py:18-70 sliding windows, NCHW input.
+#include "nqk_common.h"
+
+namespace nqk {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------------------
+// int8 MFMA GEMM: C[b][m][n] = sum_k A[m][k] * Bt[n][k]; block tile 128x128, BK = 64,
+// 4 waves (2x2), each wave 64x64 = 2x2 tiles of v_mfma_i32_32x32x32_i8.
+// LDS rows are 64 B (4 chunks of 16 B); chunk c of row r sits at c ^ ((r >> 2) & 3) so
+// that every ds_read_b128 lane group touches 16 distinct 16-B bank slots.
+constexpr int BM = 128, BN = 128, BK = 64;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+__global__ void __launch_bounds__(256)
+k_qgemm_i8(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int32_t* __restrict__ C,
+           int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, BatchMap bm,
+           int64_t a_ms, int64_t b_ms, int64_t c_ms, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[2 * (BM + BN) * BK];
+  // buffer `buf`: A tile at smem + buf*(BM+BN)*BK, B tile right after it
+#define AS(buf) (smem + (buf) * (BM + BN) * BK)
+#define BS(buf) (smem + (buf) * (BM + BN) * BK + BM * BK)
+
+  const int64_t bz = blockIdx.z;
+  A += map_a(bm, bz) * a_ms;
+  Bt += map_b(bm, bz) * b_ms;
+  C += bz * c_ms;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // staging: 512 chunks of 16 B per operand tile, 2 per thread
+  v4i ra[2], rb[2];
+  auto load_tile = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int idx = tid + i * 256, row = idx >> 2, ch = idx & 3;
+      int64_t kk = k0 + ch * 16;
+      int64_t gm = m0 + row, gn = n0 + row;
+      v4i za = {0, 0, 0, 0};
+      ra[i] = (gm < M && kk < K) ? *reinterpret_cast<const v4i*>(A + gm * lda + kk) : za;
+      rb[i] = (gn < N && kk < K) ? *reinterpret_cast<const v4i*>(Bt + gn * ldb + kk) : za;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int idx = tid + i * 256, row = idx >> 2, ch = idx & 3;
+      *reinterpret_cast<v4i*>(AS(buf) + swz(row, ch)) = ra[i];
+      *reinterpret_cast<v4i*>(BS(buf) + swz(row, ch)) = rb[i];
+    }
+  };
+
+  v16i acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+
+  const int nk = (int)((K + BK - 1) / BK);
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int r32 = lane & 31, half = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile((int64_t)(kt + 1) * BK);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      v4i fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const v4i*>(AS(cur) + swz(wm * 64 + i * 32 + r32, 2 * s + half));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const v4i*>(BS(cur) + swz(wn * 64 + j * 32 + r32, 2 * s + half));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      store_tile(cur ^ 1);
+    }
+    __syncthreads();
+  }
+  // C/D layout (gfx950, dtype independent): col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int64_t gn = n0 + wn * 64 + j * 32 + r32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (gm < M && gn < N) C[gm * ldc + gn] = acc[i][j][r];
+      }
+    }
+#undef AS
+#undef BS
+}
+
+// ---------------------------------------------------------------------------------------
+// generic integer GEMM (int64 accumulate): 16x16 threads, one output each, LDS k-tiles
+template <typename TA, typename TB>
+__global__ void __launch_bounds__(256)
+k_qgemm_generic(const TA* __restrict__ A, const TB* __restrict__ B, int64_t* __restrict__ C, int64_t M,
+                int64_t N, int64_t K, int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc,
+                BatchMap bm, int64_t a_ms, int64_t b_ms, int64_t c_ms) {
+  __shared__ int64_t sa[16][17], sb[16][17];
+  const int64_t bz = blockIdx.z;
+  A += map_a(bm, bz) * a_ms;
+  B += map_b(bm, bz) * b_ms;
+  C += bz * c_ms;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int64_t m = (int64_t)blockIdx.y * 16 + ty, n = (int64_t)blockIdx.x * 16 + tx;
+  int64_t acc = 0;
+  for (int64_t k0 = 0; k0 < K; k0 += 16) {
+    int64_t am = (int64_t)blockIdx.y * 16 + ty, ak = k0 + tx;
+    sa[ty][tx] = (am < M && ak < K) ? (int64_t)A[am * a_sm + ak * a_sk] : 0;
+    int64_t bk = k0 + ty, bn = (int64_t)blockIdx.x * 16 + tx;
+    sb[ty][tx] = (bk < K && bn < N) ? (int64_t)B[bk * b_sk + bn * b_sn] : 0;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) acc += sa[ty][kk] * sb[kk][tx];
+    __syncthreads();
+  }
+  if (m < M && n < N) C[m * ldc + n] = acc;
+}
+
+// ---------------------------------------------------------------------------------------
+// float32 GEMM in the reference BLAS's summation order.  64x64 tile, 256 threads,
+// 4x4 outputs per thread, LDS k-tiles of 16.  `kb` holds the K-block ends.
+struct KBlocks { int n; int64_t end[24]; };
+
+__global__ void __launch_bounds__(256)
+k_sgemm_blas(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
+             int64_t N, int64_t K, int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc,
+             BatchMap bm, int64_t a_ms, int64_t b_ms, int64_t c_ms, KBlocks kb) {
+  __shared__ float sa[16][64 + 4], sb[16][64 + 4];
+  const int64_t bz = blockIdx.z;
+  A += map_a(bm, bz) * a_ms;
+  B += map_b(bm, bz) * b_ms;
+  C += bz * c_ms;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int64_t m0 = (int64_t)blockIdx.y * 64, n0 = (int64_t)blockIdx.x * 64;
+  float acc[4][4], tot[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { acc[i][j] = 0.0f; tot[i][j] = 0.0f; }
+  int blk = 0;
+  int64_t bend = kb.end[0];
+  for (int64_t k0 = 0; k0 < K; k0 += 16) {
+    // stage A[m0..+64][k0..+16] and B[k0..+16][n0..+64]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int idx = tid + i * 256;
+      int r = idx >> 4, kk = idx & 15;   // A: 64 rows x 16 k
+      int64_t gm = m0 + r, gk = k0 + kk;
+      sa[kk][r] = (gm < M && gk < K) ? A[gm * a_sm + gk * a_sk] : 0.0f;
+      int kr = idx >> 6, cc = idx & 63;  // B: 16 k x 64 cols
+      int64_t bk = k0 + kr, bn = n0 + cc;
+      sb[kr][cc] = (bk < K && bn < N) ? B[bk * b_sk + bn * b_sn] : 0.0f;
+    }
+    __syncthreads();
+    const int kmax = (int)((K - k0) < 16 ? (K - k0) : 16);
+    for (int kk = 0; kk < kmax; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = sa[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = sb[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_fmaf(a[i], b[j], acc[i][j]);
+      if (k0 + kk + 1 == bend) {  // end of an OpenBLAS K block: C += block sum
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { tot[i][j] = tot[i][j] + acc[i][j]; acc[i][j] = 0.0f; }
+        ++blk;
+        bend = blk < kb.n ? kb.end[blk] : -1;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int64_t gm = m0 + ty * 4 + i;
+    if (gm >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int64_t gn = n0 + tx * 4 + j;
+      if (gn < N) C[gm * ldc + gn] = tot[i][j];
+    }
+  }
+}
+
+__global__ void k_im2col(const float* __restrict__ x, float* __restrict__ cols, int64_t n, int64_t c, int64_t h,
+                         int64_t w, int64_t kh, int64_t kw, int64_t ph0, int64_t pw0, int64_t sh, int64_t sw,
+                         int64_t ho, int64_t wo) {
+  const int64_t kcols = kh * kw * c;
+  const int64_t total = n * ho * wo * kcols;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    int64_t row = i / kcols, col = i - row * kcols;
+    int64_t ci = col % c, t = col / c, kj = t % kw, ki = t / kw;
+    int64_t ox = row % wo, t2 = row / wo, oy = t2 % ho, b = t2 / ho;
+    int64_t iy = oy * sh + ki - ph0, ix = ox * sw + kj - pw0;
+    float v = 0.0f;
+    if (iy >= 0 && iy < h && ix >= 0 && ix < w) v = x[((b * c + ci) * h + iy) * w + ix];
+    cols[i] = v;
+  }
+}
+
+}  // namespace
+
+// OpenBLAS level-3 K blocking (driver/level3/level3.c): GEMM_Q = 384 for SkylakeX sgemm
+static int blas_kblocks(int64_t K, KBlocks* kb) {
+  const int64_t Q = 384, U = 2;
+  int64_t ls = 0;
+  kb->n = 0;
+  while (ls < K) {
+    int64_t min_l = K - ls;
+    if (min_l >= 2 * Q) min_l = Q;
+    else if (min_l > Q) min_l = ((min_l / 2 + U - 1) / U) * U;
+    ls += min_l;
+    if (kb->n >= 24) return -1;
+    kb->end[kb->n++] = ls;
+  }
+  return 0;
+}
+
+}  // namespace nqk
+
+using namespace nqk;
+
+extern "C" int nqk_qgemm_i8(const int8_t* a, const int8_t* bt, int32_t* c, int64_t batch, int64_t M, int64_t N,
+                            int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const int64_t* bmap,
+                            int64_t a_mat_stride, int64_t b_mat_stride, int64_t c_mat_stride) {
+  if (batch <= 0 || M <= 0 || N <= 0) return 0;
+  if ((lda & 15) || (ldb & 15) || (K & 15)) return fail("nqk_qgemm_i8: lda, ldb and K must be multiples of 16");
+  if ((((uintptr_t)a) & 15) || (((uintptr_t)bt) & 15) || (a_mat_stride & 15) || (b_mat_stride & 15))
+    return fail("nqk_qgemm_i8: operands must be 16-byte aligned");
+  if (batch > 65535) return fail("nqk_qgemm_i8: batch > 65535");
+  int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+  if ((int64_t)tiles_m * tiles_n > 0x7fffffff) return fail("nqk_qgemm_i8: too many tiles");
+  BatchMap m = batch_map(bmap);
+  hipLaunchKernelGGL(k_qgemm_i8, dim3(tiles_m * tiles_n, 1, (unsigned)batch), dim3(256), 0, stream(), a, bt, c, M,
+                     N, K, lda, ldb, ldc, m, a_mat_stride, b_mat_stride, c_mat_stride, tiles_n);
+  return launch_status("nqk_qgemm_i8");
+}
+
+extern "C" int nqk_qgemm_generic(const void* a, int a_dtype, const void* b, int b_dtype, int64_t* c,
+                                 int64_t batch, int64_t M, int64_t N, int64_t K, int64_t a_sm, int64_t a_sk,
+                                 int64_t b_sk, int64_t b_sn, int64_t ldc, const int64_t* bmap,
+                                 int64_t a_mat_stride, int64_t b_mat_stride, int64_t c_mat_stride) {
+  if (batch <= 0 || M <= 0 || N <= 0) return 0;
+  if (batch > 65535 || (M + 15) / 16 > 65535) return fail("nqk_qgemm_generic: grid too large");
+  BatchMap m = batch_map(bmap);
+  dim3 grid((unsigned)((N + 15) / 16), (unsigned)((M + 15) / 16), (unsigned)batch);
+  NQK_INT_DISPATCH(a_dtype, TA,
+    NQK_INT_DISPATCH(b_dtype, TB,
+      hipLaunchKernelGGL((k_qgemm_generic<TA, TB>), grid, dim3(256), 0, stream(), (const TA*)a, (const TB*)b, c,
+                         M, N, K, a_sm, a_sk, b_sk, b_sn, ldc, m, a_mat_stride, b_mat_stride, c_mat_stride)));
+  return launch_status("nqk_qgemm_generic");
+}
+
+extern "C" int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch, int64_t M, int64_t N, int64_t K,
+                         int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc, const int64_t* bmap,
+                         int64_t a_mat_stride, int64_t b_mat_stride, int64_t c_mat_stride) {
+  if (batch <= 0 || M <= 0 || N <= 0) return 0;
+  if (batch > 65535 || (M + 63) / 64 > 65535) return fail("nqk_sgemm: grid too large");
+  KBlocks kb;
+  if (K <= 0) { kb.n = 0; kb.end[0] = -1; }
+  else if (blas_kblocks(K, &kb)) return fail("nqk_sgemm: K too large for the BLAS blocking table");
+  BatchMap m = batch_map(bmap);
+  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64), (unsigned)batch);
+  hipLaunchKernelGGL(k_sgemm_blas, grid, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk, b_sk, b_sn, ldc, m,
+                     a_mat_stride, b_mat_stride, c_mat_stride, kb);
+  return launch_status("nqk_sgemm");
+}
+
+extern "C" int nqk_im2col(const float* x, float* cols, int64_t n, int64_t c, int64_t h, int64_t w, int64_t kh,
+                          int64_t kw, int64_t ph0, int64_t pw0, int64_t sh, int64_t sw, int64_t ho, int64_t wo) {
+  int64_t total = n * ho * wo * kh * kw * c;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(k_im2col, dim3(grid_for(total)), dim3(kThreads), 0, stream(), x, cols, n, c, h, w, kh, kw, ph0,
+                     pw0, sh, sw, ho, wo);
+  return launch_status("nqk_im2col");
+}

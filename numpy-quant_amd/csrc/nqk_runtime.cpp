@@ -1,0 +1,104 @@
+// Runtime half of the C ABI: device selection, the per-device stream, memory,
+// timers and hipGraph capture (include/nqk.h "runtime").
+#include "nqk_common.h"
+
+#include <mutex>
+#include <string>
+
+namespace {
+thread_local std::string g_err;
+int g_device = -1;
+hipStream_t g_streams[64] = {};
+hipEvent_t g_t0 = nullptr, g_t1 = nullptr;
+hipGraph_t g_capturing = nullptr;
+std::mutex g_mu;
+}  // namespace
+
+namespace nqk {
+int fail(const std::string& msg) { g_err = msg; return -1; }
+int check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return 0;
+  return fail(std::string(what) + ": " + hipGetErrorString(e));
+}
+hipStream_t stream() {
+  if (g_device < 0) nqk_init(0);
+  return g_streams[g_device];
+}
+}  // namespace nqk
+
+using namespace nqk;
+
+extern "C" {
+
+const char* nqk_last_error(void) { return g_err.c_str(); }
+
+int nqk_device_count(int* count) { return check(hipGetDeviceCount(count), "hipGetDeviceCount"); }
+
+int nqk_init(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (device < 0 || device >= 64) return fail("bad device index");
+  if (check(hipSetDevice(device), "hipSetDevice")) return -1;
+  if (!g_streams[device]) {
+    if (check(hipStreamCreateWithFlags(&g_streams[device], hipStreamNonBlocking), "hipStreamCreate")) return -1;
+  }
+  g_device = device;
+  if (!g_t0) {
+    if (check(hipEventCreate(&g_t0), "hipEventCreate") || check(hipEventCreate(&g_t1), "hipEventCreate")) return -1;
+  }
+  return 0;
+}
+
+int nqk_malloc(void** ptr, size_t bytes) {
+  if (g_device < 0 && nqk_init(0)) return -1;
+  return check(hipMalloc(ptr, bytes ? bytes : 16), "hipMalloc");
+}
+int nqk_free(void* ptr) { return check(hipFree(ptr), "hipFree"); }
+
+int nqk_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  if (!bytes) return 0;
+  if (check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream()), "memcpy h2d")) return -1;
+  return check(hipStreamSynchronize(stream()), "memcpy h2d sync");
+}
+int nqk_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  if (!bytes) return 0;
+  if (check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream()), "memcpy d2h")) return -1;
+  return check(hipStreamSynchronize(stream()), "memcpy d2h sync");
+}
+int nqk_memcpy_d2d(void* dst, const void* src, size_t bytes) {
+  if (!bytes) return 0;
+  return check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream()), "memcpy d2d");
+}
+int nqk_memset(void* ptr, int value, size_t bytes) {
+  if (!bytes) return 0;
+  return check(hipMemsetAsync(ptr, value, bytes, stream()), "memset");
+}
+int nqk_sync(void) { return check(hipStreamSynchronize(stream()), "hipStreamSynchronize"); }
+int nqk_stream(void** s) { *s = (void*)stream(); return 0; }
+
+int nqk_timer_start(void) { return check(hipEventRecord(g_t0, stream()), "hipEventRecord"); }
+int nqk_timer_stop(void) { return check(hipEventRecord(g_t1, stream()), "hipEventRecord"); }
+int nqk_timer_ms(float* ms) {
+  if (check(hipEventSynchronize(g_t1), "hipEventSynchronize")) return -1;
+  return check(hipEventElapsedTime(ms, g_t0, g_t1), "hipEventElapsedTime");
+}
+
+int nqk_graph_begin(void) {
+  return check(hipStreamBeginCapture(stream(), hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+}
+int nqk_graph_end(void** graph_exec) {
+  hipGraph_t g = nullptr;
+  if (check(hipStreamEndCapture(stream(), &g), "hipStreamEndCapture")) return -1;
+  hipGraphExec_t ex = nullptr;
+  if (check(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0), "hipGraphInstantiate")) return -1;
+  (void)hipGraphDestroy(g);
+  *graph_exec = (void*)ex;
+  return 0;
+}
+int nqk_graph_launch(void* graph_exec) {
+  return check(hipGraphLaunch((hipGraphExec_t)graph_exec, stream()), "hipGraphLaunch");
+}
+int nqk_graph_destroy(void* graph_exec) {
+  return check(hipGraphExecDestroy((hipGraphExec_t)graph_exec), "hipGraphExecDestroy");
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+"""ctypes binding of libnqk.so (include/nqk.h).
+
+The library is built in-tree by `__graft_entry__.build()` (csrc/Makefile) and
+sits next to this file.  There is no fallback: if it is missing or fails to load,
+every entry point raises, so a silent CPU path can never stand in for the kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnqk.so")
+
+NQK_I8, NQK_I16, NQK_I32, NQK_I64, NQK_F32 = 1, 2, 3, 4, 5
+ZP_NONE, ZP_SCALAR, ZP_ROW, ZP_COL, ZP_KCONST, ZP_FULL = 0, 1, 2, 4, 8, 16
+ADD, SUB, MUL, DIV = 0, 1, 2, 3
+NEG, EXP, ERF, SQRT, RELU, SIGMOID, RECIP, TANH = range(8)
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_l = ctypes.c_int64
+_f = ctypes.c_float
+_lp = ctypes.POINTER(ctypes.c_int64)
+
+SIGNATURES = {
+    "nqk_init": [_i],
+    "nqk_device_count": [ctypes.POINTER(_i)],
+    "nqk_malloc": [ctypes.POINTER(_p), ctypes.c_size_t],
+    "nqk_free": [_p],
+    "nqk_memcpy_h2d": [_p, _p, ctypes.c_size_t],
+    "nqk_memcpy_d2h": [_p, _p, ctypes.c_size_t],
+    "nqk_memcpy_d2d": [_p, _p, ctypes.c_size_t],
+    "nqk_memset": [_p, _i, ctypes.c_size_t],
+    "nqk_sync": [],
+    "nqk_stream": [ctypes.POINTER(_p)],
+    "nqk_timer_start": [],
+    "nqk_timer_stop": [],
+    "nqk_timer_ms": [ctypes.POINTER(_f)],
+    "nqk_graph_begin": [],
+    "nqk_graph_end": [ctypes.POINTER(_p)],
+    "nqk_graph_launch": [_p],
+    "nqk_graph_destroy": [_p],
+    "nqk_quantize": [_p, _p, _i, _l, _f, _l, _i, _i, _p, _l],
+    "nqk_dequantize": [_p, _i, _p, _l, _l, _l, _f, _i, _l, _l, _l, _l, _p, _p, _lp],
+    "nqk_requantize": [_p, _i, _p, _i, _p, _i, _l, _l, _l, _f, _i, _l, _l, _l, _l, _p, _p, _lp, _f, _l, _i, _i],
+    "nqk_rowsum": [_p, _i, _p, _l, _l, _l, _l, _l],
+    "nqk_qgemm_i8": [_p, _p, _p, _l, _l, _l, _l, _l, _l, _l, _lp, _l, _l, _l],
+    "nqk_qgemm_generic": [_p, _i, _p, _i, _p, _l, _l, _l, _l, _l, _l, _l, _l, _l, _lp, _l, _l, _l],
+    "nqk_sgemm": [_p, _p, _p, _l, _l, _l, _l, _l, _l, _l, _l, _l, _lp, _l, _l, _l],
+    "nqk_im2col": [_p, _p] + [_l] * 12,
+    "nqk_binary_f32": [_i, _p, _p, _p, _i, _lp, _lp, _lp],
+    "nqk_unary_f32": [_i, _p, _p, _l],
+    "nqk_add_scalar_f32": [_p, _f, _p, _l],
+    "nqk_softmax_lastdim": [_p, _p, _l, _l],
+    "nqk_layernorm_lastdim": [_p, _p, _p, _p, _l, _l, _f],
+    "nqk_mean_lastdim": [_p, _p, _l, _l],
+    "nqk_minmax_f32": [_p, _l, _p, _p, _l],
+    "nqk_copy_strided": [_p, _p, _i, _i, _lp, _lp, _lp],
+    "nqk_where_f32": [_p, _p, _p, _p, _i, _lp, _lp, _lp, _lp],
+    "nqk_comm_unique_id": [_p],
+    "nqk_comm_init": [_p, _i, _i],
+    "nqk_comm_bcast": [_p, ctypes.c_size_t, _i],
+    "nqk_comm_gather": [_p, _p, ctypes.c_size_t, _i],
+    "nqk_comm_barrier": [],
+    "nqk_comm_destroy": [],
+}
+
+
+class NQKError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libnqk.so once and declare every exported signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NQKError(f"libnqk.so not built ({LIB_PATH}); run __graft_entry__.build() — "
+                       "there is no CPU fallback for the hot path")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    lib.nqk_last_error.argtypes = []
+    lib.nqk_last_error.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise NQKError(f"{name}: {lib.nqk_last_error().decode(errors='replace')}")
+
+
+def i64arr(values) -> ctypes.Array:
+    vals = [int(v) for v in values]
+    return (ctypes.c_int64 * max(1, len(vals)))(*vals)
+
+
+_initialised = -1
+
+
+def ensure_init(device: int | None = None) -> None:
+    global _initialised
+    if device is None:
+        device = int(os.environ.get("NQK_DEVICE", os.environ.get("LOCAL_RANK", "0")) or 0)
+        if _initialised >= 0:
+            return
+    if _initialised == device:
+        return
+    call("nqk_init", device)
+    _initialised = device
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    call("nqk_device_count", ctypes.byref(n))
+    return n.value

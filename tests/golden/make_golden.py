@@ -274,7 +274,7 @@ def gen_vit_part(out_dir, fname, tag, batch, bit_widths=(8, 4), seed=0, keep_sma
         hashes = {}
         for name, (kind, arr) in vals.items():
             hashes[name] = [kind, list(arr.shape), _h(arr)]
-            if keep_small and arr.size <= 300_000 and kind != "I":
+            if keep_small and arr.size <= 40_000 and kind != "I":
                 arrays[f"bw{bw}|{kind}|{name}"] = arr
         meta[f"bw{bw}"] = {"qparams": qparams_json(qmodel.quant_params), "hashes": hashes,
                            "ref_seconds": dt, "profile": prof}

@@ -1,0 +1,128 @@
+"""GPU parity, kernels: numpy-exact float building blocks and the integer GEMMs on
+shapes beyond the golden vectors (odd sizes, batches, broadcasts, ViT shapes),
+against NumPy on the same seeded inputs."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def init():
+    from numpy_quant import _lib
+    _lib.ensure_init()
+
+
+def test_exp_matches_numpy_on_64M_floats():
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant import kernels as K
+    rng = np.random.default_rng(7)
+    bits = rng.integers(0, 2 ** 32, size=1 << 24, dtype=np.uint64).astype(np.uint32)
+    dense = np.linspace(-110, 100, 1 << 22, dtype=np.float32)
+    for x in (bits.view(np.float32), dense):
+        y = K.unary(_lib.EXP, DeviceArray.from_host(x)).to_host()
+        with np.errstate(all="ignore"):
+            ref = np.exp(x)
+        same = (y.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(y) & np.isnan(ref))
+        assert same.all(), (x[~same][:5], y[~same][:5], ref[~same][:5])
+
+
+@pytest.mark.parametrize("rows,cols", [(7, 5), (33, 128), (64, 197), (17, 768), (9, 3072), (3, 1000), (2, 129)])
+def test_pairwise_softmax_layernorm(rows, cols):
+    from numpy_quant.tensor import FTensor
+    from numpy_quant.model import onnx_operator_implementation as op
+    rng = np.random.default_rng(rows * cols)
+    x = (rng.standard_normal((rows, cols)) * 3).astype(np.float32)
+    g = (1 + 0.02 * rng.standard_normal(cols)).astype(np.float32)
+    b = (0.02 * rng.standard_normal(cols)).astype(np.float32)
+    sm = op("Softmax", [FTensor(x)], {"axis": -1})[0].data
+    m = x + (-x.max(axis=-1, keepdims=True))
+    e = np.exp(m)
+    np.testing.assert_array_equal(sm, e / e.sum(axis=-1, keepdims=True))
+    ln = op("LayerNormalization", [FTensor(x), FTensor(g), FTensor(b)], {"axis": -1, "epsilon": 1e-12})[0].data
+    mean = x.mean(axis=-1, keepdims=True)
+    d = x + (-mean)
+    var = (d * d).mean(axis=-1, keepdims=True)
+    ref = d * (np.float32(1) / np.sqrt(var + np.float32(1e-12))) * g + b
+    np.testing.assert_array_equal(ln, ref)
+    np.testing.assert_array_equal(FTensor(x).mean(-1, keepdims=True).data, x.mean(-1, keepdims=True))
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (5, 3, 2), (100, 5, 2), (197, 768, 768), (256, 100, 700),
+                                   (130, 70, 500), (64, 300, 384), (3, 1000, 768)])
+def test_sgemm_matches_blas(M, N, K):
+    from numpy_quant.tensor import FTensor
+    rng = np.random.default_rng(M + N + K)
+    a = rng.standard_normal((M, K), dtype=np.float32)
+    b = rng.standard_normal((K, N), dtype=np.float32)
+    got = FTensor(a).matmul(FTensor(b)).data
+    ref = np.matmul(a, b)
+    if M == 1 or N == 1:  # NumPy uses gemv there: not the gemm summation order
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+    else:
+        np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("shape_a,shape_b", [((197, 768), (768, 768)), ((2, 197, 768), (768, 3072)),
+                                             ((4, 12, 197, 64), (4, 12, 64, 197)), ((4, 12, 197, 197), (4, 12, 197, 64)),
+                                             ((33, 17), (17, 45)), ((2, 1, 40, 48), (1, 2, 48, 40)),
+                                             ((129, 3072), (3072, 130))])
+@pytest.mark.parametrize("zps", [(None, None), (-9, None), (None, 5), (-138, 11)])
+def test_int8_gemm_and_zero_point_terms(shape_a, shape_b, zps):
+    from numpy_quant import numpy_quantization as nq
+    rng = np.random.default_rng(sum(shape_a) + sum(shape_b))
+    a = rng.integers(-128, 128, size=shape_a, dtype=np.int64)
+    b = rng.integers(-128, 128, size=shape_b, dtype=np.int64)
+    za = None if zps[0] is None else np.array(zps[0], np.int64)
+    zb = None if zps[1] is None else np.array(zps[1], np.int64)
+    acc, s, z = nq.q_matmul(a, np.float32(0.5), za, b, np.float32(0.25), zb)
+    np.testing.assert_array_equal(acc, np.matmul(a, b))
+    if za is None and zb is None:
+        assert z is None
+    else:
+        ra = a.sum(axis=-1, keepdims=True)
+        cb = b.sum(axis=-2, keepdims=True)
+        if za is None:
+            ref = ra * zb
+        elif zb is None:
+            ref = cb * za
+        else:
+            ref = ra * zb + cb * za - za * zb * a.shape[-1]
+        np.testing.assert_array_equal(z, ref)
+        d = nq.dequantize(acc, np.float32(0.125), z)
+        np.testing.assert_array_equal(d, ((acc - ref) * np.float32(0.125)).astype(np.float32))
+
+
+def test_wide_bit_width_gemm():
+    from numpy_quant import numpy_quantization as nq
+    rng = np.random.default_rng(3)
+    a = rng.integers(-2 ** 15, 2 ** 15, size=(37, 50), dtype=np.int64)
+    b = rng.integers(-2 ** 15, 2 ** 15, size=(50, 29), dtype=np.int64)
+    acc, _, z = nq.q_matmul(a, np.float32(1), np.array(7, np.int64), b, np.float32(1), None)
+    np.testing.assert_array_equal(acc, a @ b)
+    np.testing.assert_array_equal(z, b.sum(axis=-2, keepdims=True) * 7)
+
+
+def test_quantize_rowsum_and_graph_capture():
+    from numpy_quant import _lib, kernels as K
+    from numpy_quant.device import DeviceArray
+    import ctypes
+    rng = np.random.default_rng(11)
+    x = (rng.standard_normal((300, 197)) * 4).astype(np.float32)
+    dx = DeviceArray.from_host(x)
+    q, rs = K.quantize(dx, 8, np.float32(0.05), -3, rowsum=True)
+    qh = q.to_host().astype(np.int64)
+    from oracle import nq_oracle as O
+    ref = O.quantize(x, 8, np.array(0.05, np.float32), np.array(-3, np.int64))
+    np.testing.assert_array_equal(qh, ref)
+    np.testing.assert_array_equal(rs.to_host(), ref.sum(axis=-1))
+    # capture the same quantize into a hipGraph and replay it
+    out = DeviceArray(x.shape, np.int8)
+    _lib.call("nqk_graph_begin")
+    _lib.call("nqk_quantize", dx.vp, out.vp, out.code, x.size, float(np.float32(0.05)), -3, 1, 8, None, 197)
+    g = ctypes.c_void_p()
+    _lib.call("nqk_graph_end", ctypes.byref(g))
+    _lib.call("nqk_graph_launch", g)
+    np.testing.assert_array_equal(out.to_host().astype(np.int64), ref)
+    _lib.call("nqk_graph_destroy", g)
