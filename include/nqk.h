@@ -66,6 +66,11 @@ int nqk_stream(void** stream);         /* the library's hipStream_t */
 int nqk_timer_start(void);
 int nqk_timer_stop(void);
 int nqk_timer_ms(float* ms);
+/* events on the library stream (per-kernel timing inside bench.py) */
+int nqk_event_create(void** event);
+int nqk_event_record(void* event);
+int nqk_event_elapsed(void* start, void* stop, float* ms);   /* waits for stop */
+int nqk_event_destroy(void* event);
 /* hipGraph capture of everything issued between begin and end */
 int nqk_graph_begin(void);
 int nqk_graph_end(void** graph_exec);

@@ -82,6 +82,19 @@ int nqk_timer_ms(float* ms) {
   return check(hipEventElapsedTime(ms, g_t0, g_t1), "hipEventElapsedTime");
 }
 
+int nqk_event_create(void** event) {
+  hipEvent_t e = nullptr;
+  if (check(hipEventCreate(&e), "hipEventCreate")) return -1;
+  *event = (void*)e;
+  return 0;
+}
+int nqk_event_record(void* event) { return check(hipEventRecord((hipEvent_t)event, stream()), "hipEventRecord"); }
+int nqk_event_elapsed(void* start, void* stop, float* ms) {
+  if (check(hipEventSynchronize((hipEvent_t)stop), "hipEventSynchronize")) return -1;
+  return check(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop), "hipEventElapsedTime");
+}
+int nqk_event_destroy(void* event) { return check(hipEventDestroy((hipEvent_t)event), "hipEventDestroy"); }
+
 int nqk_graph_begin(void) {
   return check(hipStreamBeginCapture(stream(), hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
 }

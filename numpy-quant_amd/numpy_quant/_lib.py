@@ -37,6 +37,10 @@ SIGNATURES = {
     "nqk_timer_start": [],
     "nqk_timer_stop": [],
     "nqk_timer_ms": [ctypes.POINTER(_f)],
+    "nqk_event_create": [ctypes.POINTER(_p)],
+    "nqk_event_record": [_p],
+    "nqk_event_elapsed": [_p, _p, ctypes.POINTER(_f)],
+    "nqk_event_destroy": [_p],
     "nqk_graph_begin": [],
     "nqk_graph_end": [ctypes.POINTER(_p)],
     "nqk_graph_launch": [_p],

@@ -160,6 +160,46 @@ def batch_map(a_batch, b_batch):
 MFMA_MIN_WORK = 1 << 15
 
 
+class KernelTimer:
+    """Brackets selected kernel launches with stream events (bench.py roofline):
+    `records` collects (tag, start_event, stop_event, work) tuples."""
+
+    def __init__(self):
+        self.records = []
+        self._free = []
+
+    def _event(self):
+        if self._free:
+            return self._free.pop()
+        e = ctypes.c_void_p()
+        _lib.call("nqk_event_create", ctypes.byref(e))
+        return e
+
+    def begin(self):
+        e = self._event()
+        _lib.call("nqk_event_record", e)
+        return e
+
+    def end(self, tag, start, work):
+        e = self._event()
+        _lib.call("nqk_event_record", e)
+        self.records.append((tag, start, e, work))
+
+    def collect(self):
+        """[(tag, ms, work)] and recycle the events."""
+        out = []
+        for tag, a, b, w in self.records:
+            ms = ctypes.c_float()
+            _lib.call("nqk_event_elapsed", a, b, ctypes.byref(ms))
+            out.append((tag, ms.value, w))
+            self._free += [a, b]
+        self.records = []
+        return out
+
+
+TIMER: KernelTimer | None = None
+
+
 def _pad_k(x: DeviceArray, rows_shape, k: int, kp: int) -> DeviceArray:
     """Copy [..., rows, k] into a zero-filled [..., rows, kp] (kp % 16 == 0)."""
     out = DeviceArray(tuple(rows_shape) + (kp,), x.dtype).fill_zero()
@@ -207,8 +247,11 @@ def qmatmul(a: DeviceArray, b: DeviceArray, zpa, zpb, b_transposed: DeviceArray 
         else:
             bt = b_transposed
         acc = DeviceArray(out_batch + (M, N), np.int32)
+        t0 = TIMER.begin() if TIMER is not None else None
         _lib.call("nqk_qgemm_i8", ap.vp, bt.vp, acc.vp, nb, M, N, kp, kp, kp, N, _lib.i64arr(bmap),
                   M * kp, N * kp, M * N)
+        if t0 is not None:
+            TIMER.end("qgemm_i8", t0, (2 * nb * M * N * K, nb * (M * K + N * K + 4 * M * N)))
     else:
         acc = DeviceArray(out_batch + (M, N), np.int64)
         _lib.call("nqk_qgemm_generic", a.vp, a.code, b.vp, b.code, acc.vp, nb, M, N, K, K, 1, N, 1, N,

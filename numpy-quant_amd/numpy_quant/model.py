@@ -222,6 +222,22 @@ class Model:
         outputs = [value_dict[vi.name] for vi in graph.output]
         return cls(list(nodes.values()), list(value_dict.values()), inputs, outputs)
 
+    def rebatch(self, batch: int) -> int:
+        """Rewrite the batch-1 int64 shape constants of a torch export in place
+        (onnx_proto.rebatch).  A QModel built from this model
+        shares its nodes' attribute dicts, so either one may be rebatched."""
+        if not hasattr(self, "_batch1_consts"):
+            self._batch1_consts = {id(n): n.attrs.get("value") for n in self.nodes if n.op == "Constant"}
+        count = 0
+        for node in self.nodes:
+            v = self._batch1_consts.get(id(node))
+            if isinstance(v, np.ndarray) and v.dtype == np.int64 and v.ndim == 1 and v.shape[0] in (3, 4) and v[0] == 1:
+                v = v.copy()
+                v[0] = batch
+                node.attrs["value"] = v
+                count += 1
+        return count
+
     def _set_inputs(self, inputs):
         for array, variable in zip(inputs, self.inputs):
             if array.dtype == np.float32:
@@ -247,11 +263,9 @@ class Model:
         result = [out.data.data for out in self.outputs]
         return (result, times) if profile else result
 
-    def quantize(self, calibration_inputs: list[np.ndarray], bit_width=8):
-        """Calibration + graph rewrite (model.py:328-442); min/max on device."""
+    def calibrate(self, calibration_inputs: list[np.ndarray]) -> tuple[dict, dict]:
+        """Float forward + per-value global min / max (model.py:329-336), min/max on device."""
         self(calibration_inputs)
-        node_dict = {node.name: node for node in self.nodes}
-        value_dict = {value.name: value for value in self.values}
         vmin, vmax = {}, {}
         for val in self.values:
             t = val.data
@@ -262,10 +276,27 @@ class Model:
                 d = t.data
                 flat = d.reshape((d.shape[0], -1) if d.shape else (-1,))
                 vmin[val.name], vmax[val.name] = np.mean(flat.min()), np.mean(flat.max())
+        return vmin, vmax
+
+    def quantize(self, calibration_inputs: list[np.ndarray], bit_width=8):
+        """Calibration + graph rewrite (model.py:328-442)."""
+        vmin, vmax = self.calibrate(calibration_inputs)
 
         def params(value: Value, asym: bool):
             s, z = quant_parameters(vmin[value.name], vmax[value.name], bit_width=bit_width, asymmetric=asym)
             return QuantizationParams(s, z)
+
+        return self._rewrite(bit_width, params)
+
+    def quantize_with(self, quant_params: dict, bit_width=8):
+        """The graph rewrite of Model.quantize with given per-value quantization
+        parameters (e.g. calibrated on a smaller batch, or the reference's own),
+        skipping the calibration forward."""
+        return self._rewrite(bit_width, lambda value, asym: quant_params[value.name])
+
+    def _rewrite(self, bit_width, params):
+        node_dict = {node.name: node for node in self.nodes}
+        value_dict = {value.name: value for value in self.values}
 
         qnodes: OrderedDict[str, Node] = OrderedDict()
         qvalues: dict[str, Value] = {}
