@@ -71,7 +71,7 @@ def build_qmodel(batch: int, bit_width: int, calib_batch: int = 8):
     for v in model.values:
         if v.__class__.__name__ == "Variable":
             v.data = None
-    qmodel.rebatch(batch)
+    model.rebatch(batch)  # shared attribute dicts: rebatches the QModel too
     return model, qmodel
 
 

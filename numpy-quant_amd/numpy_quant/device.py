@@ -197,8 +197,21 @@ def collapse(shape, *stride_sets):
     return shp, strides
 
 
+def _check_range(arr: DeviceArray, elem_offset: int, shape, strides, what: str) -> None:
+    """Host-side bounds check of a strided access against the array's block: a bad
+    view must raise here, never reach the GPU as an out-of-bounds access."""
+    if any(int(s) == 0 for s in shape):
+        return
+    lo = elem_offset + sum((int(n) - 1) * int(st) for n, st in zip(shape, strides) if int(st) < 0)
+    hi = elem_offset + sum((int(n) - 1) * int(st) for n, st in zip(shape, strides) if int(st) > 0)
+    if lo < 0 or hi + 1 > arr.size:
+        raise ValueError(f"{what}: strided access [{lo}, {hi}] outside the buffer of {arr.shape} {arr.dtype}")
+
+
 def copy_strided(src: DeviceArray, dst: DeviceArray, shape, src_strides, dst_strides,
                  src_offset: int = 0, dst_offset: int = 0) -> None:
+    _check_range(src, src_offset, shape, src_strides, "copy source")
+    _check_range(dst, dst_offset, shape, dst_strides, "copy destination")
     shp, (ss, ds) = collapse(shape, src_strides, dst_strides)
     if len(shp) > 6:
         raise ValueError("copy of more than 6 non-mergeable dimensions")

@@ -224,13 +224,14 @@ class Model:
 
     def rebatch(self, batch: int) -> int:
         """Rewrite the batch-1 int64 shape constants of a torch export in place
-        (onnx_proto.rebatch).  A QModel built from this model
-        shares its nodes' attribute dicts, so either one may be rebatched."""
-        if not hasattr(self, "_batch1_consts"):
-            self._batch1_consts = {id(n): n.attrs.get("value") for n in self.nodes if n.op == "Constant"}
+        (onnx_proto.rebatch).  The batch-1 original is kept in
+        the node's attribute dict, which a QModel built from this model shares, so
+        either one may be rebatched any number of times."""
         count = 0
         for node in self.nodes:
-            v = self._batch1_consts.get(id(node))
+            if node.op != "Constant":
+                continue
+            v = node.attrs.setdefault("__batch1_value__", node.attrs.get("value"))
             if isinstance(v, np.ndarray) and v.dtype == np.int64 and v.ndim == 1 and v.shape[0] in (3, 4) and v[0] == 1:
                 v = v.copy()
                 v[0] = batch

@@ -344,6 +344,10 @@ def concat(x_list: list[Tensor], axis: int):
     devs = [x.dev for x in x_list]
     nd = devs[0].ndim
     axis %= nd
+    for d in devs[1:]:
+        if d.ndim != nd or any(d.shape[k] != devs[0].shape[k] for k in range(nd) if k != axis):
+            raise ValueError("all the input array dimensions except for the concatenation axis must match "
+                             f"exactly ({devs[0].shape} vs {d.shape}, axis {axis})")
     out_shape = list(devs[0].shape)
     out_shape[axis] = sum(d.shape[axis] for d in devs)
     out = DeviceArray(out_shape, np.float32)

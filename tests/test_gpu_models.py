@@ -89,6 +89,9 @@ def tainted_values(model):
                 bad.update(o.name for o in node.outputs)
         if any(i in bad for i in ins):
             bad.update(o.name for o in node.outputs)
+            # constants quantized with a tainted value's scale (Gemm / Add biases at 4*bw)
+            if node.op in ("Gemm", "Add"):
+                bad.update(i.name for i in node.inputs if i.__class__.__name__ == "Constant")
     return bad
 
 
