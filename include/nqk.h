@@ -169,6 +169,42 @@ int nqk_where_f32(const int64_t* cond, const float* a, const float* b, float* ou
                   const int64_t* shape, const int64_t* c_strides, const int64_t* a_strides,
                   const int64_t* b_strides);
 
+/* ------------------------------------------- fused device plan (plan.py) */
+/* Epilogue of nqk_qgemm_fused: the consumer chain of a q_matmul output as the
+ * reference's node loop runs it (dequantize -> float ops -> quantize), per element. */
+enum nqk_epi { NQK_EPI_QKV = 0, NQK_EPI_SCORES = 1, NQK_EPI_PV = 2, NQK_EPI_RESID = 3, NQK_EPI_GELU = 4 };
+typedef struct nqk_epilogue {
+  int32_t zp_flags, bit_width, group_cols, tokens, heads, hdim, ld_out, pad0;
+  int64_t zpa, zpb, kdim;              /* zero-point term as in nqk_dequantize         */
+  const int64_t* row;
+  const int64_t* col;
+  float s_acc[3];                       /* dequant scale s_a*s_b per column group       */
+  float s_out[3];                       /* quantize scale of the consumer value         */
+  int64_t zp_out[3];                    /* quantize zero point of the consumer value    */
+  void* out[3];                         /* outputs per column group                     */
+  const float* bias;                    /* dequantized bias [N] (EPI_QKV/RESID/GELU)    */
+  const float* resid;                   /* residual [M][N] (EPI_RESID)                  */
+  float div, add1, mul2, pad1;          /* Div constant (8 / sqrt 2), GELU +1 and *0.5  */
+} nqk_epilogue;
+/* int8 MFMA GEMM C = A . Bt^T (layouts as nqk_qgemm_i8) with a fused epilogue:
+ *   QKV    model.py MatMul -> Add(bias) -> Reshape -> Transpose -> quantize, 3 groups
+ *   SCORES MatMul(Q, K^T) -> Div(const)                          -> f32
+ *   PV     MatMul(P, V) -> Transpose -> Reshape -> quantize      -> int8
+ *   RESID  MatMul -> Add(bias) -> Add(residual)                  -> f32
+ *   GELU   MatMul -> Add(bias) -> Div -> Erf -> Add -> Mul -> Mul -> quantize */
+int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, int64_t M, int64_t N, int64_t K,
+                    int64_t lda, int64_t ldb, const int64_t* bmap, int64_t a_mat_stride, int64_t b_mat_stride,
+                    const nqk_epilogue* params);
+/* LayerNormalization (model.py:134-152) fused with the consumer MatMul's quantize */
+int nqk_ln_quant(const float* x, const float* gamma, const float* beta, int8_t* out, int64_t rows, int64_t cols,
+                 float eps, float scale, int64_t zp, int bit_width);
+/* Softmax (tensor.py:211-218) fused with quantize; out row stride ldo (zero pad), int64 row sums */
+int nqk_softmax_quant(const float* x, int8_t* out, int64_t* rowsum, int64_t rows, int64_t cols, int64_t ldo,
+                      float scale, int64_t zp, int bit_width);
+/* int8 [nb][R][C] -> [nb][C][Rp] (zero padded) and rowsum[nb][C] = sum over R (may be NULL) */
+int nqk_transpose_pad_i8(const int8_t* src, int8_t* dst, int64_t* rowsum, int64_t nb, int64_t R, int64_t C,
+                         int64_t Rp);
+
 /* ------------------------------------------------ multi-GPU replicas (RCCL) */
 int nqk_comm_unique_id(void* id128);                         /* rank 0 */
 int nqk_comm_init(const void* id128, int nranks, int rank);

@@ -1,0 +1,135 @@
+// NumPy-exact float building blocks shared by nqk_float.hip and nqk_fused.hip:
+// numpy's AVX512F float32 exp, the reference's A&S erf (numpy_helper.py:95-112) and
+// NumPy's pairwise summation plan (used by mean / sum / LayerNorm / Softmax).
+#pragma once
+#include "nqk_common.h"
+
+namespace nqk {
+namespace {
+
+// ------------------------------------------------------------------ numpy float32 exp
+__device__ __forceinline__ float np_expf(float x) {
+  const float xmax = 88.72283935546875f, xmin = -103.97208404541015625f;
+  if (x != x) return x;
+  const bool over = x >= xmax, under = x <= xmin;
+  float xx = (over || under) ? 0.0f : x;
+  float q = xx * 1.442695040888963407359924681001892137f;
+  q = q + 0x1.800000p+23f;
+  q = q - 0x1.800000p+23f;
+  float r = __builtin_fmaf(q, -6.93145752e-1f, xx);
+  r = __builtin_fmaf(q, -1.42860677e-6f, r);
+  r = __builtin_fmaf(q, 0.0f, r);
+  float num = __builtin_fmaf(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);
+  num = __builtin_fmaf(num, r, 5.114512081637298353406e-02f);
+  num = __builtin_fmaf(num, r, 2.473615434895520810817e-01f);
+  num = __builtin_fmaf(num, r, 7.257664613233124478488e-01f);
+  num = __builtin_fmaf(num, r, 9.999999999980870924916e-01f);
+  float den = __builtin_fmaf(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
+  den = __builtin_fmaf(den, r, 1.0f);
+  float poly = num / den;
+  poly = __builtin_ldexpf(poly, (int)q);
+  if (over) poly = __builtin_inff();
+  if (under) poly = 0.0f;
+  return poly;
+}
+
+// numpy_helper.py:95-112 (A&S 7.1.26), float32 throughout
+__device__ __forceinline__ float ref_erf(float x) {
+  float sgn = (x > 0.0f) ? 1.0f : ((x < 0.0f) ? -1.0f : (x == 0.0f ? 0.0f : x));
+  float ax = __builtin_fabsf(x);
+  float t = 1.0f / (1.0f + 0.3275911f * ax);
+  float p = 1.061405429f * t + -1.453152027f;
+  p = p * t;
+  p = p + 1.421413741f;
+  p = p * t + -0.284496736f;
+  p = p * t + 0.254829592f;
+  float y = 1.0f - p * t * np_expf(-ax * ax);
+  return sgn * y;
+}
+
+// ------------------------------------------------------------------ NumPy pairwise sum
+// The recursion of NumPy's pairwise_sum (n < 8: sequential; n <= 128: 8 interleaved
+// accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the n % 8 tail;
+// else split at n/2 rounded down to a multiple of 8) depends only on n, so the host
+// flattens it into leaves + a post-order combine program shared by every row.
+constexpr int kMaxLeaves = 64;
+struct PwPlan {
+  int nleaf, nops;
+  int start[kMaxLeaves], len[kMaxLeaves];
+  signed char ops[2 * kMaxLeaves];  // >= 0: push leaf; -1: pop b, pop a, push a + b
+};
+
+static int build_plan(int64_t n, int64_t s, PwPlan& p) {
+  if (n <= 128) {
+    if (p.nleaf >= kMaxLeaves) return -1;
+    p.start[p.nleaf] = (int)s;
+    p.len[p.nleaf] = (int)n;
+    p.ops[p.nops++] = (signed char)p.nleaf++;
+    return 0;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  if (build_plan(n2, s, p) || build_plan(n - n2, s + n2, p)) return -1;
+  p.ops[p.nops++] = -1;
+  return 0;
+}
+
+// one 64-lane block per row; `v` is the row in LDS, scratch holds 8 partials per leaf
+__device__ float row_pairwise_sum(const float* v, const PwPlan& p, float* part, float* leafv) {
+  const int lane = threadIdx.x;
+  for (int c = lane; c < p.nleaf * 8; c += 64) {
+    int l = c >> 3, j = c & 7;
+    int L = p.len[l], s = p.start[l];
+    float r = 0.0f;
+    if (L >= 8) {
+      r = v[s + j];
+      int end = L - (L % 8);
+      for (int i = 8 + j; i < end; i += 8) r = r + v[s + i];
+    }
+    part[c] = r;
+  }
+  __syncthreads();
+  for (int l = lane; l < p.nleaf; l += 64) {
+    int L = p.len[l], s = p.start[l];
+    float res;
+    if (L < 8) {
+      res = 0.0f;
+      for (int i = 0; i < L; ++i) res = res + v[s + i];
+    } else {
+      const float* r = part + l * 8;
+      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      for (int i = L - (L % 8); i < L; ++i) res = res + v[s + i];
+    }
+    leafv[l] = res;
+  }
+  __syncthreads();
+  float* total = leafv + kMaxLeaves;
+  if (lane == 0) {
+    float st[16];
+    int sp = 0;
+    for (int o = 0; o < p.nops; ++o) {
+      int op = p.ops[o];
+      if (op >= 0) st[sp++] = leafv[op];
+      else { float b = st[--sp]; float a = st[--sp]; st[sp++] = a + b; }
+    }
+    *total = st[0];
+  }
+  __syncthreads();
+  float t = *total;
+  __syncthreads();
+  return t;
+}
+
+int row_plan(int64_t cols, PwPlan& p) {
+  p.nleaf = 0;
+  p.nops = 0;
+  if (cols <= 0 || build_plan(cols, 0, p)) return fail("row length not supported by the pairwise-sum plan (max 8192)");
+  return 0;
+}
+
+
+static size_t row_smem(int64_t cols) { return (size_t)(cols + kMaxLeaves * 8 + kMaxLeaves + 4) * sizeof(float); }
+static unsigned row_grid(int64_t rows) { return (unsigned)(rows < 65536 * 4 ? rows : 65536 * 4); }
+
+}  // namespace
+}  // namespace nqk

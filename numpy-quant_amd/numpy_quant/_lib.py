@@ -23,6 +23,19 @@ _l = ctypes.c_int64
 _f = ctypes.c_float
 _lp = ctypes.POINTER(ctypes.c_int64)
 
+class Epilogue(ctypes.Structure):
+    """Mirror of `nqk_epilogue` (include/nqk.h)."""
+    _fields_ = [("zp_flags", ctypes.c_int32), ("bit_width", ctypes.c_int32), ("group_cols", ctypes.c_int32),
+                ("tokens", ctypes.c_int32), ("heads", ctypes.c_int32), ("hdim", ctypes.c_int32),
+                ("ld_out", ctypes.c_int32), ("pad0", ctypes.c_int32),
+                ("zpa", ctypes.c_int64), ("zpb", ctypes.c_int64), ("kdim", ctypes.c_int64),
+                ("row", ctypes.c_void_p), ("col", ctypes.c_void_p),
+                ("s_acc", ctypes.c_float * 3), ("s_out", ctypes.c_float * 3), ("zp_out", ctypes.c_int64 * 3),
+                ("out", ctypes.c_void_p * 3), ("bias", ctypes.c_void_p), ("resid", ctypes.c_void_p),
+                ("div", ctypes.c_float), ("add1", ctypes.c_float), ("mul2", ctypes.c_float),
+                ("pad1", ctypes.c_float)]
+
+
 SIGNATURES = {
     "nqk_init": [_i],
     "nqk_device_count": [ctypes.POINTER(_i)],
@@ -62,6 +75,10 @@ SIGNATURES = {
     "nqk_minmax_f32": [_p, _l, _p, _p, _l],
     "nqk_copy_strided": [_p, _p, _i, _i, _lp, _lp, _lp],
     "nqk_where_f32": [_p, _p, _p, _p, _i, _lp, _lp, _lp, _lp],
+    "nqk_qgemm_fused": [_i, _p, _p, _l, _l, _l, _l, _l, _l, _lp, _l, _l, ctypes.POINTER(Epilogue)],
+    "nqk_ln_quant": [_p, _p, _p, _p, _l, _l, _f, _f, _l, _i],
+    "nqk_softmax_quant": [_p, _p, _p, _l, _l, _l, _f, _l, _i],
+    "nqk_transpose_pad_i8": [_p, _p, _p, _l, _l, _l, _l],
     "nqk_comm_unique_id": [_p],
     "nqk_comm_init": [_p, _i, _i],
     "nqk_comm_bcast": [_p, ctypes.c_size_t, _i],

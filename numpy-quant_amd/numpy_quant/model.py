@@ -413,44 +413,63 @@ class QModel(Model):
             else:
                 raise ValueError(f"Array dtype {array.dtype} not supported")
 
+    def compile(self):
+        """Build the fused device plan (plan.py): matched transformer layers run as
+        fused launches with bit-identical results; everything else stays eager.
+        Values inside fused layers are not materialised (their `.data` is None)."""
+        from .plan import compile_plan
+        self._plan = compile_plan(self)
+        return self._plan
+
+    def _run_node(self, node, times, profile=False):
+        """One iteration of the node loop of QModel.__call__ (model.py:502-550)."""
+        args = []
+        if node.op in ("MatMul", "Gemm"):
+            for i in node.inputs:
+                if isinstance(i.data, FTensor):
+                    qp = self.quant_params[i.name]
+                    t0 = time()
+                    args.append(quantize_tensor(i.data, self.bit_width, qp.scale, qp.zero_point))
+                    if profile:
+                        sync()
+                    if times is not None:
+                        times["TinyqQuant"] += time() - t0
+                else:
+                    args.append(i.data)
+        else:
+            for i in node.inputs:
+                if isinstance(i.data, QTensor):
+                    t0 = time()
+                    args.append(self._dequant_input(i))
+                    if profile:
+                        sync()
+                    if times is not None:
+                        times["TinyqDequant"] += time() - t0
+                else:
+                    args.append(i.data)
+        t0 = time()
+        outs = onnx_operator_implementation(node.op, args, node.attrs)
+        if node.op == "Gemm":
+            qp = self.quant_params[node.outputs[0].name]
+            outs = [t.requantize(self.bit_width, qp.scale, qp.zero_point) for t in outs]
+        if profile:
+            sync()
+        if times is not None:
+            times[node.op] += time() - t0
+        for o, tensor in zip(node.outputs, outs):
+            o.data = tensor
+
     def run(self, profile=False):
-        """The node loop of QModel.__call__ (model.py:497-550) on device tensors."""
+        """The node loop of QModel.__call__ (model.py:497-550) on device tensors,
+        through the fused plan when `compile()` was called."""
         times = {op: 0.0 for op in {n.op for n in self.nodes}}
         times["TinyqQuant"] = 0.0
         times["TinyqDequant"] = 0.0
-        for node in self.nodes:
-            args = []
-            if node.op in ("MatMul", "Gemm"):
-                for i in node.inputs:
-                    if isinstance(i.data, FTensor):
-                        qp = self.quant_params[i.name]
-                        t0 = time()
-                        args.append(quantize_tensor(i.data, self.bit_width, qp.scale, qp.zero_point))
-                        if profile:
-                            sync()
-                        times["TinyqQuant"] += time() - t0
-                    else:
-                        args.append(i.data)
-            else:
-                for i in node.inputs:
-                    if isinstance(i.data, QTensor):
-                        t0 = time()
-                        args.append(self._dequant_input(i))
-                        if profile:
-                            sync()
-                        times["TinyqDequant"] += time() - t0
-                    else:
-                        args.append(i.data)
-            t0 = time()
-            outs = onnx_operator_implementation(node.op, args, node.attrs)
-            if node.op == "Gemm":
-                qp = self.quant_params[node.outputs[0].name]
-                outs = [t.requantize(self.bit_width, qp.scale, qp.zero_point) for t in outs]
-            if profile:
-                sync()
-            times[node.op] += time() - t0
-            for o, tensor in zip(node.outputs, outs):
-                o.data = tensor
+        if self._plan is not None:
+            self._plan.run(self, times, profile)
+        else:
+            for node in self.nodes:
+                self._run_node(node, times, profile)
         return times
 
     def outputs_device(self) -> list[FTensor]:

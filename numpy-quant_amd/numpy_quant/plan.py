@@ -1,0 +1,448 @@
+"""Fused device plan for QModel.__call__ (numpy_quant/model.py:486-565).
+
+`compile_plan(qmodel)` pattern-matches the transformer encoder layers of the
+graph (the ViT exports in models/vit/) and replaces each layer's ~40 nodes by
+11 fused launches (nqk_ln_quant, nqk_qgemm_fused with QKV / SCORES / PV / RESID /
+GELU epilogues, nqk_softmax_quant, row sums and an int8 transpose).  Every other
+node runs through the eager node loop.  Each fused launch performs, per element,
+the same dequantize -> float ops -> quantize sequence as the node loop, so the
+layer output is bit-identical to the eager path (tests/test_gpu_plan.py); the
+layer's intermediate values are not materialised (their `.data` stays None).
+
+Matching is strict: any deviation in ops, attributes, wiring or constants leaves
+the layer to the eager loop.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from . import kernels as KM
+from .device import DeviceArray
+from .tensor import FTensor, QTensor
+
+EPI_QKV, EPI_SCORES, EPI_PV, EPI_RESID, EPI_GELU = 0, 1, 2, 3, 4
+
+
+Epilogue = _lib.Epilogue
+
+
+class NoMatch(Exception):
+    pass
+
+
+def _f32(x) -> float:
+    return float(np.float32(x))
+
+
+def _zp(p) -> int:
+    if p.zero_point is None:
+        raise NoMatch("asymmetric parameters expected")
+    return int(p.zero_point)
+
+
+# ----------------------------------------------------------------------------- matching helpers
+def _only(lst, what):
+    if len(lst) != 1:
+        raise NoMatch(f"{what}: expected one, got {len(lst)}")
+    return lst[0]
+
+
+def _consumer(value, op):
+    n = _only(value.outputs, f"consumer of {value.name}")
+    if n.op != op:
+        raise NoMatch(f"{value.name} feeds {n.op}, expected {op}")
+    return n
+
+
+def _const_node_value(value):
+    """Value produced by a Constant node (e.g. the Div by 8.0) -> (numpy array, node)."""
+    if value.__class__.__name__ != "Variable" or len(value.inputs) != 1 or value.inputs[0].op != "Constant":
+        raise NoMatch(f"{value.name} is not a Constant-node output")
+    node = value.inputs[0]
+    return node.attrs["value"], node
+
+
+def _is_const(v):
+    return v.__class__.__name__ == "Constant"
+
+
+def _matmul_weight(node):
+    a, w = node.inputs
+    if not _is_const(w) or _is_const(a):
+        raise NoMatch("MatMul with a constant weight expected")
+    return a, w
+
+
+def _bias_add(mm_out):
+    add = _consumer(mm_out, "Add")
+    consts = [i for i in add.inputs if _is_const(i)]
+    if len(consts) != 1:
+        raise NoMatch("bias Add expected")
+    return add, consts[0]
+
+
+class LayerMatch:
+    """Values / constants of one encoder layer (names as in the QModel)."""
+
+    def __init__(self, qmodel, ln1):
+        self.nodes = set()
+        take = self.nodes.add
+        take(ln1)
+        self.ln1 = ln1
+        self.x_in = ln1.inputs[0]
+        if ln1.attrs.get("axis", -1) not in (-1, 2):
+            raise NoMatch("LayerNorm axis")
+        ln1_out = ln1.outputs[0]
+        mms = ln1_out.outputs
+        if len(mms) != 3 or any(m.op != "MatMul" for m in mms):
+            raise NoMatch("LN1 must feed three MatMuls")
+        roles = {}
+        for mm in mms:
+            take(mm)
+            _, w = _matmul_weight(mm)
+            add, bias = _bias_add(mm.outputs[0])
+            take(add)
+            rs = _consumer(add.outputs[0], "Reshape")
+            take(rs)
+            shp_val, shp_node = _const_node_value(rs.inputs[1])
+            take(shp_node)
+            tr = _consumer(rs.outputs[0], "Transpose")
+            take(tr)
+            perm = list(tr.attrs["perm"])
+            nxt = _only(tr.outputs[0].outputs, "transpose consumer")
+            if nxt.op != "MatMul":
+                raise NoMatch("head transpose must feed a MatMul")
+            idx = nxt.inputs.index(tr.outputs[0])
+            if perm == [0, 2, 3, 1] and idx == 1:
+                role = "k"
+            elif perm == [0, 2, 1, 3] and idx == 0:
+                role = "q"
+            elif perm == [0, 2, 1, 3] and idx == 1:
+                role = "v"
+            else:
+                raise NoMatch(f"unexpected head layout {perm}/{idx}")
+            if role in roles:
+                raise NoMatch("duplicate role")
+            roles[role] = dict(mm=mm, w=w, bias=bias, shape=np.asarray(shp_val), tr_out=tr.outputs[0], user=nxt)
+        if set(roles) != {"q", "k", "v"}:
+            raise NoMatch("q/k/v roles")
+        self.roles = roles
+        scores = roles["q"]["user"]
+        if roles["k"]["user"] is not scores:
+            raise NoMatch("Q and K must meet in one MatMul")
+        take(scores)
+        div = _consumer(scores.outputs[0], "Div")
+        take(div)
+        dval, dnode = _const_node_value(div.inputs[1])
+        if div.inputs[0] is not scores.outputs[0] or np.asarray(dval).size != 1:
+            raise NoMatch("scores Div")
+        take(dnode)
+        self.div = _f32(np.asarray(dval).reshape(()))
+        sm = _consumer(div.outputs[0], "Softmax")
+        take(sm)
+        if sm.attrs.get("axis") not in (-1, 3):
+            raise NoMatch("softmax axis")
+        pv = _consumer(sm.outputs[0], "MatMul")
+        if pv is not roles["v"]["user"] or pv.inputs[0] is not sm.outputs[0]:
+            raise NoMatch("PV MatMul wiring")
+        take(pv)
+        tr3 = _consumer(pv.outputs[0], "Transpose")
+        take(tr3)
+        if list(tr3.attrs["perm"]) != [0, 2, 1, 3]:
+            raise NoMatch("context transpose")
+        rs3 = _consumer(tr3.outputs[0], "Reshape")
+        take(rs3)
+        _, rs3c = _const_node_value(rs3.inputs[1])
+        take(rs3c)
+        dense = _consumer(rs3.outputs[0], "MatMul")
+        take(dense)
+        _, self.wo = _matmul_weight(dense)
+        add_o, self.bo = _bias_add(dense.outputs[0])
+        take(add_o)
+        res1 = _consumer(add_o.outputs[0], "Add")
+        take(res1)
+        if self.x_in not in res1.inputs:
+            raise NoMatch("attention residual")
+        x1 = res1.outputs[0]
+        users = x1.outputs
+        if len(users) != 2:
+            raise NoMatch("x1 must feed LN2 and the second residual")
+        ln2 = next((u for u in users if u.op == "LayerNormalization"), None)
+        res2_candidates = [u for u in users if u.op == "Add"]
+        if ln2 is None or len(res2_candidates) != 1:
+            raise NoMatch("LN2 / residual 2")
+        take(ln2)
+        self.ln2 = ln2
+        up = _consumer(ln2.outputs[0], "MatMul")
+        take(up)
+        _, self.w1 = _matmul_weight(up)
+        add_u, self.b1 = _bias_add(up.outputs[0])
+        take(add_u)
+        h = add_u.outputs[0]
+        hu = h.outputs
+        gdiv = next((u for u in hu if u.op == "Div"), None)
+        gmul = next((u for u in hu if u.op == "Mul"), None)
+        if len(hu) != 2 or gdiv is None or gmul is None or gdiv.inputs[0] is not h:
+            raise NoMatch("GELU structure")
+        take(gdiv)
+        v, n = _const_node_value(gdiv.inputs[1])
+        take(n)
+        self.gelu_div = _f32(np.asarray(v).reshape(()))
+        erf = _consumer(gdiv.outputs[0], "Erf")
+        take(erf)
+        gadd = _consumer(erf.outputs[0], "Add")
+        take(gadd)
+        other = [i for i in gadd.inputs if i is not erf.outputs[0]]
+        v, n = _const_node_value(_only(other, "gelu +1 operand"))
+        take(n)
+        self.gelu_add = _f32(np.asarray(v).reshape(()))
+        if gmul.inputs[0] is not h or gmul.inputs[1] is not gadd.outputs[0]:
+            raise NoMatch("GELU Mul operand order")
+        take(gmul)
+        gmul2 = _consumer(gmul.outputs[0], "Mul")
+        take(gmul2)
+        if gmul2.inputs[0] is not gmul.outputs[0]:
+            raise NoMatch("GELU Mul_1 operand order")
+        v, n = _const_node_value(gmul2.inputs[1])
+        take(n)
+        self.gelu_mul = _f32(np.asarray(v).reshape(()))
+        self.h_out = gmul2.outputs[0]
+        down = _consumer(self.h_out, "MatMul")
+        take(down)
+        _, self.w2 = _matmul_weight(down)
+        add_d, self.b2 = _bias_add(down.outputs[0])
+        take(add_d)
+        res2 = _consumer(add_d.outputs[0], "Add")
+        if res2 is not res2_candidates[0] or x1 not in res2.inputs:
+            raise NoMatch("FFN residual")
+        take(res2)
+        self.x_out = res2.outputs[0]
+        self.ln1_out, self.ln2_out = ln1_out, ln2.outputs[0]
+        self.sm_out, self.rs3_out = sm.outputs[0], rs3.outputs[0]
+        # every intermediate value must be private to the layer
+        for node in self.nodes:
+            for o in node.outputs:
+                if o is self.x_out:
+                    continue
+                for u in o.outputs:
+                    if u not in self.nodes:
+                        raise NoMatch(f"{o.name} escapes the layer")
+        shp = roles["q"]["shape"]
+        if shp.size != 4 or any((roles[r]["shape"][1:] != shp[1:]).any() for r in "kv"):
+            raise NoMatch("head reshape")
+        self.tokens, self.heads, self.hdim = int(shp[1]), int(shp[2]), int(shp[3])
+
+
+# ----------------------------------------------------------------------------- fused layer
+class FusedLayer:
+    def __init__(self, qmodel, m: LayerMatch):
+        self.m = m
+        self.bw = qmodel.bit_width
+        qp = qmodel.quant_params
+        deq = qmodel._dequant_input
+        self.g1, self.be1 = deq(m.ln1.inputs[1]).dev, deq(m.ln1.inputs[2]).dev
+        self.g2, self.be2 = deq(m.ln2.inputs[1]).dev, deq(m.ln2.inputs[2]).dev
+        self.eps1 = _f32(m.ln1.attrs.get("epsilon", 1e-5))
+        self.eps2 = _f32(m.ln2.attrs.get("epsilon", 1e-5))
+        self.p_ln1, self.p_ln2 = qp[m.ln1_out.name], qp[m.ln2_out.name]
+        self.p_sm, self.p_ctx, self.p_h = qp[m.sm_out.name], qp[m.rs3_out.name], qp[m.h_out.name]
+        self.p_head = {r: qp[m.roles[r]["tr_out"].name] for r in "qkv"}
+        # weights: pre-transposed int8 Bt, column sums, dequantized biases
+        bts, cols, biases, self.s_w = [], [], [], {}
+        for r in "qkv":
+            w = m.roles[r]["w"].data
+            bt, col = w.weight_operand()
+            bts.append(bt)
+            cols.append(col)
+            biases.append(deq(m.roles[r]["bias"]).dev)
+            self.s_w[r] = w.scale
+        self.D = bts[0].shape[1]
+        if any(b.shape[1] != self.D or b.dtype != np.int8 for b in bts):
+            raise NoMatch("int8 weights with a common K expected")
+        self.bt_qkv = _cat0(bts)
+        self.col_qkv = _cat0(cols)
+        self.bias_qkv = _cat0(biases)
+        self.bt_o, self.col_o = m.wo.data.weight_operand()
+        self.bt_1, self.col_1 = m.w1.data.weight_operand()
+        self.bt_2, self.col_2 = m.w2.data.weight_operand()
+        self.s_wo, self.s_w1, self.s_w2 = m.wo.data.scale, m.w1.data.scale, m.w2.data.scale
+        self.bias_o, self.bias_1, self.bias_2 = deq(m.bo).dev, deq(m.b1).dev, deq(m.b2).dev
+        self.F = self.bt_1.shape[0]
+        if self.D != m.heads * m.hdim or self.bt_o.shape != (self.D, self.D) or self.bt_2.shape != (self.D, self.F):
+            raise NoMatch("layer dimensions")
+
+    def _epi(self, **kw) -> Epilogue:
+        e = Epilogue()
+        e.bit_width = self.bw
+        e.group_cols = kw.pop("group_cols", 1 << 30)
+        e.tokens, e.heads, e.hdim = self.m.tokens, self.m.heads, self.m.hdim
+        e.div, e.add1, e.mul2 = kw.pop("div", 1.0), kw.pop("add1", 0.0), kw.pop("mul2", 1.0)
+        for k, v in kw.items():
+            if k in ("s_acc", "s_out", "zp_out", "out"):
+                arr = getattr(e, k)
+                for i, x in enumerate(v):
+                    arr[i] = x
+            else:
+                setattr(e, k, v)
+        return e
+
+    def run(self, ws: "Workspace"):
+        m, bw = self.m, self.bw
+        x = m.x_in.data
+        if not isinstance(x, FTensor):
+            raise ValueError("fused layer input must be a float tensor")
+        B, T, D = x.dev.shape
+        if T != m.tokens or D != self.D:
+            raise ValueError(f"layer input {x.dev.shape} does not match the graph ({m.tokens}, {self.D})")
+        H, Dh, F = m.heads, m.hdim, self.F
+        Mrows = B * T
+        Tp = (T + 15) // 16 * 16
+        w = ws.get(B, T, Tp, H, Dh, D, F)
+        call = _lib.call
+        # 1) LN1 + quantize (LN1 output feeds the Q/K/V MatMuls)
+        call("nqk_ln_quant", x.dev.vp, self.g1.vp, self.be1.vp, w["lnq"].vp, Mrows, D, self.eps1,
+             _f32(self.p_ln1.scale), _zp(self.p_ln1), bw)
+        # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
+        s_a = np.float32(self.p_ln1.scale)
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), col=self.col_qkv.ptr, group_cols=D,
+                      s_acc=[_f32(s_a * np.float32(self.s_w[r])) for r in "qkv"],
+                      s_out=[_f32(self.p_head[r].scale) for r in "qkv"],
+                      zp_out=[_zp(self.p_head[r]) for r in "qkv"],
+                      out=[w["q"].ptr, w["k"].ptr, w["v"].ptr], bias=self.bias_qkv.ptr)
+        _gemm(EPI_QKV, w["lnq"], self.bt_qkv, 1, Mrows, 3 * D, D, D, D, None, 0, 0, e)
+        # 3) zero-point row / column sums of the attention operands
+        call("nqk_rowsum", w["q"].vp, _lib.NQK_I8, w["qrs"].vp, 1, B * H * T, Dh, Dh, 0)
+        call("nqk_rowsum", w["k"].vp, _lib.NQK_I8, w["krs"].vp, 1, B * H * T, Dh, Dh, 0)
+        call("nqk_transpose_pad_i8", w["v"].vp, w["vt"].vp, w["vcs"].vp, B * H, T, Dh, Tp)
+        # 4) scores = dequant(Q K^T) / 8
+        pq, pk, pv_ = self.p_head["q"], self.p_head["k"], self.p_head["v"]
+        e = self._epi(zp_flags=_lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST, zpa=_zp(pq), zpb=_zp(pk), kdim=Dh,
+                      row=w["qrs"].ptr, col=w["krs"].ptr,
+                      s_acc=[_f32(np.float32(pq.scale) * np.float32(pk.scale))], out=[w["s"].ptr], div=m.div)
+        _gemm(EPI_SCORES, w["q"], w["k"], B * H, T, T, Dh, Dh, Dh, None, T * Dh, T * Dh, e)
+        # 5) softmax + quantize (+ row sums for the PV zero-point term)
+        call("nqk_softmax_quant", w["s"].vp, w["p"].vp, w["prs"].vp, B * H * T, T, Tp,
+             _f32(self.p_sm.scale), _zp(self.p_sm), bw)
+        # 6) context = dequant(P V) -> Transpose -> Reshape -> quantize
+        e = self._epi(zp_flags=_lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST, zpa=_zp(self.p_sm), zpb=_zp(pv_), kdim=T,
+                      row=w["prs"].ptr, col=w["vcs"].ptr,
+                      s_acc=[_f32(np.float32(self.p_sm.scale) * np.float32(pv_.scale))],
+                      s_out=[_f32(self.p_ctx.scale)], zp_out=[_zp(self.p_ctx)], out=[w["ctx"].ptr], ld_out=D)
+        _gemm(EPI_PV, w["p"], w["vt"], B * H, T, Dh, Tp, Tp, Tp, None, T * Tp, Dh * Tp, e)
+        # 7) output projection + bias + residual
+        x1 = DeviceArray((B, T, D), np.float32)
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr,
+                      s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
+                      resid=x.dev.ptr, out=[x1.ptr])
+        _gemm(EPI_RESID, w["ctx"], self.bt_o, 1, Mrows, D, D, D, D, None, 0, 0, e)
+        # 8) LN2 + quantize
+        call("nqk_ln_quant", x1.vp, self.g2.vp, self.be2.vp, w["ln2q"].vp, Mrows, D, self.eps2,
+             _f32(self.p_ln2.scale), _zp(self.p_ln2), bw)
+        # 9) FFN up + bias + GELU + quantize
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr,
+                      s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
+                      s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[w["h"].ptr],
+                      div=m.gelu_div, add1=m.gelu_add, mul2=m.gelu_mul)
+        _gemm(EPI_GELU, w["ln2q"], self.bt_1, 1, Mrows, F, D, D, D, None, 0, 0, e)
+        # 10) FFN down + bias + residual
+        x2 = DeviceArray((B, T, D), np.float32)
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr,
+                      s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
+                      resid=x1.ptr, out=[x2.ptr])
+        _gemm(EPI_RESID, w["h"], self.bt_2, 1, Mrows, D, F, F, F, None, 0, 0, e)
+        m.x_out.data = FTensor(x2)
+
+
+def _cat0(arrs):
+    """Concatenate contiguous device arrays along axis 0."""
+    shape = (sum(a.shape[0] for a in arrs),) + tuple(arrs[0].shape[1:])
+    out = DeviceArray(shape, arrs[0].dtype)
+    off = 0
+    for a in arrs:
+        _lib.call("nqk_memcpy_d2d", ctypes.c_void_p(out.ptr + off), a.vp, a.nbytes)
+        off += a.nbytes
+    return out
+
+
+def _gemm(epi, a, bt, batch, M, N, K, lda, ldb, bmap, a_ms, b_ms, e):
+    if K % 16 or lda % 16 or ldb % 16:
+        raise ValueError("fused GEMM operands must be 16-byte padded")
+    need_a = (batch - 1) * a_ms + (M - 1) * lda + K if batch > 1 else (M - 1) * lda + K
+    need_b = (batch - 1) * b_ms + (N - 1) * ldb + K if batch > 1 else (N - 1) * ldb + K
+    if need_a > a.size or need_b > bt.size:
+        raise ValueError("fused GEMM operand smaller than its shape")
+    t0 = KM.TIMER.begin() if KM.TIMER is not None else None
+    _lib.call("nqk_qgemm_fused", epi, a.vp, bt.vp, batch, M, N, K, lda, ldb,
+              _lib.i64arr(bmap) if bmap is not None else None, a_ms, b_ms, ctypes.byref(e))
+    if t0 is not None:
+        KM.TIMER.end("qgemm_fused", t0, (2 * batch * M * N * K, batch * (M * K + N * K)))
+
+
+class Workspace:
+    """Scratch buffers of a fused layer, shared by all layers of one plan."""
+
+    def __init__(self):
+        self.key = None
+        self.bufs = {}
+
+    def get(self, B, T, Tp, H, Dh, D, F):
+        key = (B, T, Tp, H, Dh, D, F)
+        if key != self.key:
+            M = B * T
+            self.bufs = {
+                "lnq": DeviceArray((M, D), np.int8), "ln2q": DeviceArray((M, D), np.int8),
+                "q": DeviceArray((B * H * T, Dh), np.int8), "k": DeviceArray((B * H * T, Dh), np.int8),
+                "v": DeviceArray((B * H * T, Dh), np.int8), "vt": DeviceArray((B * H, Dh, Tp), np.int8),
+                "qrs": DeviceArray((B * H * T,), np.int64), "krs": DeviceArray((B * H * T,), np.int64),
+                "vcs": DeviceArray((B * H * Dh,), np.int64), "s": DeviceArray((B * H, T, T), np.float32),
+                "p": DeviceArray((B * H, T, Tp), np.int8), "prs": DeviceArray((B * H * T,), np.int64),
+                "ctx": DeviceArray((M, D), np.int8), "h": DeviceArray((M, F), np.int8),
+            }
+            self.key = key
+        return self.bufs
+
+
+class Plan:
+    """Ordered steps: eager nodes and fused layers."""
+
+    def __init__(self, qmodel):
+        self.steps = []
+        self.ws = Workspace()
+        self.fused = 0
+        claimed = {}
+        if qmodel.bit_width <= 8 and qmodel.bit_width >= 2:
+            for node in qmodel.nodes:
+                if node.op != "LayerNormalization" or node in claimed:
+                    continue
+                try:
+                    m = LayerMatch(qmodel, node)
+                    layer = FusedLayer(qmodel, m)
+                except NoMatch:
+                    continue
+                for n in m.nodes:
+                    claimed[n] = layer
+        placed = set()
+        for node in qmodel.nodes:
+            layer = claimed.get(node)
+            if layer is None:
+                self.steps.append(("node", node))
+            elif id(layer) not in placed:
+                placed.add(id(layer))
+                self.steps.append(("layer", layer))
+                self.fused += 1
+
+    def run(self, qmodel, times=None, profile=False):
+        for kind, obj in self.steps:
+            if kind == "node":
+                qmodel._run_node(obj, times, profile)
+            else:
+                obj.run(self.ws)
+
+
+def compile_plan(qmodel) -> Plan:
+    return Plan(qmodel)

@@ -1,0 +1,57 @@
+"""GPU parity of the fused device plan (plan.py): the fused encoder layers must
+reproduce the eager node loop — and therefore the reference — bit for bit."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+MODELS = os.path.join(ROOT, "numpy-quant_amd", "models")
+
+
+def _vit(batch, seed=0):
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model
+    proto = onnx_proto.load(os.path.join(MODELS, "vit_image_classifier_no_weights.onnx"), synthetic_weights=True,
+                            seed=seed)
+    if batch != 1:
+        onnx_proto.rebatch(proto, batch)
+    return Model.from_onnx(proto)
+
+
+def test_plan_matches_reference_vit_b1():
+    from test_gpu_models import ref_qparams
+    meta = json.load(open(os.path.join(GOLDEN, "vit_b1.json")))
+    arrs = np.load(os.path.join(GOLDEN, "vit_b1.npz"))
+    model = _vit(1, meta["seed"])
+    qmodel = model.quantize_with(ref_qparams(meta["bw8"]["qparams"]), bit_width=8)
+    plan = qmodel.compile()
+    assert plan.fused == 12
+    out = qmodel([arrs["x_run"]])[0]
+    np.testing.assert_array_equal(out, arrs["bw8_out"])
+    # every layer output (residual stream) equals the reference's value
+    hashes = meta["bw8"]["hashes"]
+    for step, layer in [s for s in plan.steps if s[0] == "layer"]:
+        v = layer.m.x_out
+        arr = np.ascontiguousarray(v.data.data)
+        assert hashlib.sha256(arr.tobytes()).hexdigest() == hashes[v.name][2], v.name
+
+
+@pytest.mark.parametrize("batch,bw", [(3, 8), (2, 4)])
+def test_plan_equals_eager(batch, bw):
+    rng = np.random.default_rng(batch)
+    x = rng.standard_normal((batch, 3, 224, 224)).astype(np.float32)
+    model = _vit(batch)
+    qmodel = model.quantize([x], bit_width=bw)
+    eager = qmodel([x])[0]
+    layer_outs = {}
+    plan = qmodel.compile()
+    assert plan.fused == 12
+    for _, layer in [s for s in plan.steps if s[0] == "layer"]:
+        layer_outs[layer.m.x_out.name] = None
+    fused = qmodel([x])[0]
+    np.testing.assert_array_equal(fused, eager)
