@@ -200,19 +200,33 @@ __global__ void k_minmax_partial(const float* __restrict__ x, int64_t n, float* 
   }
 }
 
-__global__ void k_minmax_final(const float* __restrict__ part, int nparts, float* __restrict__ out) {
-  if (threadIdx.x != 0) return;
+__global__ void __launch_bounds__(256) k_minmax_final(const float* __restrict__ part, int nparts, float* __restrict__ out) {
   float mn = __builtin_inff(), mx = -__builtin_inff();
   bool nan = false;
-  for (int i = 0; i < nparts; ++i) {
-    float a = part[2 * i], b = part[2 * i + 1];
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+    const float a = part[2 * i], b = part[2 * i + 1];
     nan |= (a != a) || (b != b);
     mn = a < mn ? a : mn;
     mx = b > mx ? b : mx;
   }
-  if (nan) { mn = __builtin_nanf(""); mx = mn; }
-  out[0] = mn;
-  out[1] = mx;
+  for (int off = 32; off > 0; off >>= 1) {
+    const float a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const unsigned long long anynan = __ballot(nan);
+  __shared__ float smn[4], smx[4];
+  __shared__ int snan[4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[w] = mn; smx[w] = mx; snan[w] = anynan != 0; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bool nn = false;
+    for (int i = 0; i < 4; ++i) { mn = smn[i] < mn ? smn[i] : mn; mx = smx[i] > mx ? smx[i] : mx; nn |= snan[i] != 0; }
+    if (nn) { mn = __builtin_nanf(""); mx = mn; }
+    out[0] = mn;
+    out[1] = mx;
+  }
 }
 
 Nd make_nd(int ndim, const int64_t* shape, const int64_t* s0, const int64_t* s1, const int64_t* s2) {
@@ -305,7 +319,7 @@ extern "C" int nqk_minmax_f32(const float* x, int64_t n, float* out2, float* scr
   if (parts < 1) return fail("nqk_minmax_f32: scratch too small");
   unsigned g = grid_for(n, 256, parts < 2048 ? parts : 2048);
   hipLaunchKernelGGL(k_minmax_partial, dim3(g), dim3(256), 0, stream(), x, n, scratch);
-  hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(64), 0, stream(), scratch, (int)g, out2);
+  hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(256), 0, stream(), scratch, (int)g, out2);
   return launch_status("nqk_minmax_f32");
 }
 

@@ -43,12 +43,11 @@ __device__ __forceinline__ int quant_zp(float x, float s, double zp, double lo, 
 }
 
 struct Epi {
-  // zero-point term (see nqk.h): zpt = row[a(b)*M+m]*zpb + col[b(b)*N+n]*zpa - zpa*zpb*K
+  // zero-point term (see nqk.h): zpt = rowsumA[m]*zpb + rowsumBt[n]*zpa - zpa*zpb*K; the
+  // row sums of A and of Bt are accumulated inside the kernel from the staged tiles
   int zp_flags;
   int64_t zpa, zpb, kdim;
-  const int64_t* row;
-  const int64_t* col;
-  int group_cols;        // columns per output group (EPI_QKV), else N
+  int group_cols;        // columns per output group (EPI_QKV), else >= N
   float s_acc[3];        // dequant scale per group
   const float* bias;     // dequantized bias [N] or null
   float s_out[3];        // quantize scale per group
@@ -63,53 +62,21 @@ struct Epi {
 
 enum { EPI_QKV = 0, EPI_SCORES = 1, EPI_PV = 2, EPI_RESID = 3, EPI_GELU = 4 };
 
-template <int EPI>
-__device__ __forceinline__ void epi_store(const Epi& e, const BatchMap& bm, int64_t b, int64_t gm, int64_t gn,
-                                          int64_t M, int64_t N, int32_t acc) {
-  int64_t v = (int64_t)acc;
-  if (e.zp_flags & NQK_ZP_ROW) v -= e.row[map_a(bm, b) * M + gm] * e.zpb;
-  if (e.zp_flags & NQK_ZP_COL) v -= e.col[map_b(bm, b) * N + gn] * e.zpa;
-  if (e.zp_flags & NQK_ZP_KCONST) v += e.zpa * e.zpb * e.kdim;
-  const int g = (EPI == EPI_QKV) ? (int)(gn / e.group_cols) : 0;
-  const float d = (float)((double)v * (double)e.s_acc[g]);
-  if constexpr (EPI == EPI_SCORES) {
-    float* o = (float*)e.out[0];
-    o[(b * M + gm) * N + gn] = d / e.div;
-  } else if constexpr (EPI == EPI_RESID) {
-    float* o = (float*)e.out[0];
-    const int64_t i = gm * N + gn;
-    o[i] = (e.bias[gn] + d) + e.resid[i];
-  } else if constexpr (EPI == EPI_GELU) {
-    const float h = e.bias[gn] + d;
-    const float t = h / e.div;
-    const float a = ref_erf(t) + e.add1;
-    const float y = (h * a) * e.mul2;
-    int8_t* o = (int8_t*)e.out[0];
-    o[gm * N + gn] = (int8_t)quant_zp(y, e.s_out[0], e.zp_out[0], e.lo, e.hi);
-  } else if constexpr (EPI == EPI_QKV) {
-    const float h = e.bias[gn] + d;
-    const int q = quant_zp(h, e.s_out[g], e.zp_out[g], e.lo, e.hi);
-    const int64_t nl = gn - (int64_t)g * e.group_cols;
-    const int64_t img = gm / e.tokens, t = gm - img * e.tokens;
-    const int64_t hh = nl / e.hdim, dd = nl - hh * e.hdim;
-    int8_t* o = (int8_t*)e.out[g];
-    o[((img * e.heads + hh) * e.tokens + t) * e.hdim + dd] = (int8_t)q;  // [b, h, t, d]
-  } else {  // EPI_PV: batch b = img*heads + h, row = token, col = d -> ctx[img*T + t][h*D + d]
-    const int q = quant_zp(d, e.s_out[0], e.zp_out[0], e.lo, e.hi);
-    const int64_t img = b / e.heads, hh = b - img * e.heads;
-    int8_t* o = (int8_t*)e.out[0];
-    o[(img * e.tokens + gm) * (int64_t)e.ld_out + hh * e.hdim + gn] = (int8_t)q;
-  }
+__device__ __forceinline__ int sum16(v4i c) {
+  int s = __builtin_amdgcn_sdot4(c[0], 0x01010101, 0, false);
+  s = __builtin_amdgcn_sdot4(c[1], 0x01010101, s, false);
+  s = __builtin_amdgcn_sdot4(c[2], 0x01010101, s, false);
+  return __builtin_amdgcn_sdot4(c[3], 0x01010101, s, false);
 }
 
 template <int EPI>
 __global__ void __launch_bounds__(256)
-k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int64_t M, int64_t N, int64_t K,
-            int64_t lda, int64_t ldb, BatchMap bm, int64_t a_ms, int64_t b_ms, int tiles_m, int tiles_n, Epi e) {
+k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
+            BatchMap bm, int64_t a_ms, int64_t b_ms, int tiles_m, int tiles_n, Epi e) {
   __shared__ __attribute__((aligned(16))) int8_t smem[2 * (FBM + FBN) * FBK];
 #define AS(buf) (smem + (buf) * (FBM + FBN) * FBK)
 #define BS(buf) (smem + (buf) * (FBM + FBN) * FBK + FBM * FBK)
-  const int64_t bz = blockIdx.z;
+  const int bz = blockIdx.z;
   A += map_a(bm, bz) * a_ms;
   Bt += map_b(bm, bz) * b_ms;
   // XCD-aware tile order: consecutive tiles that share an A row panel land on one XCD
@@ -120,20 +87,22 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int64_t
     wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
   }
   const int tm = wg / tiles_n, tn = wg % tiles_n;
-  const int64_t m0 = (int64_t)tm * FBM, n0 = (int64_t)tn * FBN;
+  const int m0 = tm * FBM, n0 = tn * FBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  const bool need_ra = (e.zp_flags & NQK_ZP_ROW) != 0, need_rb = (e.zp_flags & NQK_ZP_COL) != 0;
 
   v4i ra[4], rb[4];
-  auto load_tile = [&](int64_t k0) {
+  int psa[4] = {0, 0, 0, 0}, psb[4] = {0, 0, 0, 0};  // partial row sums of the staged chunks
+  auto load_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + i * 256, row = idx >> 3, ch = idx & 7;
-      const int64_t kk = k0 + ch * 16;
-      const int64_t gm = m0 + row, gn = n0 + row;
+      const int kk = k0 + ch * 16;
+      const int gm = m0 + row, gn = n0 + row;
       const v4i z = {0, 0, 0, 0};
-      ra[i] = (gm < M && kk < K) ? *reinterpret_cast<const v4i*>(A + gm * lda + kk) : z;
-      rb[i] = (gn < N && kk < K) ? *reinterpret_cast<const v4i*>(Bt + gn * ldb + kk) : z;
+      ra[i] = (gm < M && kk < K) ? *reinterpret_cast<const v4i*>(A + (int64_t)gm * lda + kk) : z;
+      rb[i] = (gn < N && kk < K) ? *reinterpret_cast<const v4i*>(Bt + (int64_t)gn * ldb + kk) : z;
     }
   };
   auto store_tile = [&](int buf) {
@@ -142,6 +111,8 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int64_t
       const int idx = tid + i * 256, row = idx >> 3, ch = idx & 7;
       *reinterpret_cast<v4i*>(AS(buf) + swz128(row, ch)) = ra[i];
       *reinterpret_cast<v4i*>(BS(buf) + swz128(row, ch)) = rb[i];
+      if (need_ra) psa[i] += sum16(ra[i]);
+      if (need_rb) psb[i] += sum16(rb[i]);
     }
   };
 
@@ -153,14 +124,14 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int64_t
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
 
-  const int nk = (int)((K + FBK - 1) / FBK);
+  const int nk = (K + FBK - 1) / FBK;
   load_tile(0);
   store_tile(0);
   __syncthreads();
   const int r32 = lane & 31, half = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile((int64_t)(kt + 1) * FBK);
+    if (kt + 1 < nk) load_tile((kt + 1) * FBK);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       v4i fa[2], fb[2];
@@ -181,79 +152,157 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int64_t
   }
 #undef AS
 #undef BS
+  // row sums of the A and Bt rows of this tile (8 lanes share a row), kept in LDS
+  int* rsA = reinterpret_cast<int*>(smem);
+  int* rsB = rsA + FBM;
+  if (need_ra || need_rb) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t gn = n0 + wn * 64 + j * 32 + r32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (gm < M && gn < N) epi_store<EPI>(e, bm, bz, gm, gn, M, N, acc[i][j][r]);
+    for (int i = 0; i < 4; ++i) {
+      int sa = psa[i], sb = psb[i];
+      sa += __shfl_xor(sa, 1, 64); sa += __shfl_xor(sa, 2, 64); sa += __shfl_xor(sa, 4, 64);
+      sb += __shfl_xor(sb, 1, 64); sb += __shfl_xor(sb, 2, 64); sb += __shfl_xor(sb, 4, 64);
+      if ((tid & 7) == 0) {
+        const int row = (tid + i * 256) >> 3;
+        rsA[row] = sa;
+        rsB[row] = sb;
       }
     }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: per-column values hoisted, per-row values once per row
+  const int64_t kconst = (e.zp_flags & NQK_ZP_KCONST) ? e.zpa * e.zpb * e.kdim : 0;
+  int64_t colterm[2];
+  float bias_j[2];
+  int gcol[2], grp[2], hh_j[2], dd_j[2];
+  bool nvalid[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int nl = wn * 64 + j * 32 + r32;
+    const int gn = n0 + nl;
+    nvalid[j] = gn < N;
+    gcol[j] = gn;
+    colterm[j] = (need_rb ? (int64_t)rsB[nl] * e.zpa : 0) - kconst;
+    bias_j[j] = (e.bias != nullptr && nvalid[j]) ? e.bias[gn] : 0.0f;
+    grp[j] = 0;
+    hh_j[j] = 0;
+    dd_j[j] = gn;
+    if constexpr (EPI == EPI_QKV) {
+      grp[j] = gn / e.group_cols;
+      const int nloc = gn - grp[j] * e.group_cols;
+      hh_j[j] = nloc / e.hdim;
+      dd_j[j] = nloc - hh_j[j] * e.hdim;
+    }
+  }
+  int img_b = 0, head_b = 0;
+  if constexpr (EPI == EPI_PV) {
+    img_b = bz / e.heads;
+    head_b = bz - img_b * e.heads;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      const int gm = m0 + ml;
+      if (gm >= M) continue;
+      const int64_t rowterm = need_ra ? (int64_t)rsA[ml] * e.zpb : 0;
+      int img = 0, t = 0;
+      if constexpr (EPI == EPI_QKV) {
+        img = gm / e.tokens;
+        t = gm - img * e.tokens;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (!nvalid[j]) continue;
+        const int64_t v = (int64_t)acc[i][j][r] - rowterm - colterm[j];
+        const int g = grp[j];
+        const float d = (float)((double)v * (double)e.s_acc[g]);
+        const int gn = gcol[j];
+        if constexpr (EPI == EPI_SCORES) {
+          float* o = (float*)e.out[0];
+          o[((int64_t)bz * M + gm) * N + gn] = d / e.div;
+        } else if constexpr (EPI == EPI_RESID) {
+          const int64_t idx = (int64_t)gm * N + gn;
+          ((float*)e.out[0])[idx] = (bias_j[j] + d) + e.resid[idx];
+        } else if constexpr (EPI == EPI_GELU) {
+          const float h = bias_j[j] + d;
+          const float a = ref_erf(h / e.div) + e.add1;
+          const float y = (h * a) * e.mul2;
+          ((int8_t*)e.out[0])[(int64_t)gm * N + gn] = (int8_t)quant_zp(y, e.s_out[0], e.zp_out[0], e.lo, e.hi);
+        } else if constexpr (EPI == EPI_QKV) {
+          const int q = quant_zp(bias_j[j] + d, e.s_out[g], e.zp_out[g], e.lo, e.hi);
+          ((int8_t*)e.out[g])[(((int64_t)img * e.heads + hh_j[j]) * e.tokens + t) * e.hdim + dd_j[j]] = (int8_t)q;
+        } else {  // EPI_PV
+          const int q = quant_zp(d, e.s_out[0], e.zp_out[0], e.lo, e.hi);
+          ((int8_t*)e.out[0])[((int64_t)img_b * e.tokens + gm) * e.ld_out + head_b * e.hdim + gn] = (int8_t)q;
+        }
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------ LayerNorm + quantize
-__global__ void __launch_bounds__(64)
+// 4 waves per block, one row per wave; per-wave LDS slice of row_smem(cols) bytes
+__global__ void __launch_bounds__(256)
 k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
            int8_t* __restrict__ out, int64_t rows, int64_t cols, float eps, PwPlan p, float s, double zp, double lo,
-           double hi) {
+           double hi, int64_t slice) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* v = sm;
-  float* part = sm + cols;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* v = sm + w * slice;
+  float* part = v + cols;
   float* leafv = part + kMaxLeaves * 8;
-  const int lane = threadIdx.x;
   const float fcols = (float)cols;
-  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+  for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < rows; r += (int64_t)gridDim.x * 4) {
     const float* xr = x + r * cols;
     for (int64_t i = lane; i < cols; i += 64) v[i] = xr[i];
-    __syncthreads();
-    const float mean = row_pairwise_sum(v, p, part, leafv) / fcols;
+    wave_lds_sync();
+    const float mean = wave_pairwise_sum(v, p, part, leafv) / fcols;
     const float nmean = -mean;
     for (int64_t i = lane; i < cols; i += 64) {
-      float d = v[i] + nmean;
+      const float d = v[i] + nmean;
       v[i] = d * d;
     }
-    __syncthreads();
-    const float var = row_pairwise_sum(v, p, part, leafv) / fcols;
+    wave_lds_sync();
+    const float var = wave_pairwise_sum(v, p, part, leafv) / fcols;
     const float inv = 1.0f / __builtin_sqrtf(var + eps);
     int8_t* orow = out + r * cols;
     for (int64_t i = lane; i < cols; i += 64) {
-      float d = xr[i] + nmean;
-      float y = ((d * inv) * g[i]) + b[i];
+      const float d = xr[i] + nmean;
+      const float y = ((d * inv) * g[i]) + b[i];
       orow[i] = (int8_t)quant_zp(y, s, zp, lo, hi);
     }
-    __syncthreads();
+    wave_lds_sync();
   }
 }
 
 // ------------------------------------------------------------------ Softmax + quantize
-// one row per 64-lane block; output row stride ldo (>= cols, pad zero-filled), row sum
-__global__ void __launch_bounds__(64)
+// one row per wave; output row stride ldo (>= cols, pad zero-filled); optional row sums
+__global__ void __launch_bounds__(256)
 k_softmax_quant(const float* __restrict__ x, int8_t* __restrict__ out, int64_t* __restrict__ rowsum, int64_t rows,
-                int64_t cols, int64_t ldo, PwPlan p, float s, double zp, double lo, double hi) {
+                int64_t cols, int64_t ldo, PwPlan p, float s, double zp, double lo, double hi, int64_t slice) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* v = sm;
-  float* part = sm + cols;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* v = sm + w * slice;
+  float* part = v + cols;
   float* leafv = part + kMaxLeaves * 8;
-  const int lane = threadIdx.x;
-  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+  for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < rows; r += (int64_t)gridDim.x * 4) {
     const float* xr = x + r * cols;
     float mx = -__builtin_inff();
     for (int64_t i = lane; i < cols; i += 64) {
-      float t = xr[i];
+      const float t = xr[i];
       v[i] = t;
       mx = t > mx ? t : mx;
     }
     for (int off = 32; off > 0; off >>= 1) {
-      float o = __shfl_xor(mx, off, 64);
+      const float o = __shfl_xor(mx, off, 64);
       mx = o > mx ? o : mx;
     }
     const float nm = -mx;
     for (int64_t i = lane; i < cols; i += 64) v[i] = np_expf(v[i] + nm);
-    __syncthreads();
-    const float ssum = row_pairwise_sum(v, p, part, leafv);
+    wave_lds_sync();
+    const float ssum = wave_pairwise_sum(v, p, part, leafv);
     int8_t* orow = out + r * ldo;
     int64_t acc = 0;
     for (int64_t i = lane; i < ldo; i += 64) {
@@ -264,40 +313,47 @@ k_softmax_quant(const float* __restrict__ x, int8_t* __restrict__ out, int64_t* 
       }
       orow[i] = (int8_t)q;
     }
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if (lane == 0) rowsum[r] = acc;
-    __syncthreads();
+    if (rowsum) {
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (lane == 0) rowsum[r] = acc;
+    }
+    wave_lds_sync();
   }
 }
 
 // ------------------------------------------------------------------ int8 transpose + pad
-// src [nb][R][C] -> dst [nb][C][Rp] (Rp >= R, pad columns zero), rowsum[nb][C] = sum_r src
+// src [nb][R][C] -> dst [nb][C][Rp] (Rp >= R, pad zero); block = (64 columns, one matrix),
+// loops over R in 64-row tiles; optional rowsum[nb][C] = sum over R.
 __global__ void __launch_bounds__(256)
 k_transpose_pad(const int8_t* __restrict__ src, int8_t* __restrict__ dst, int64_t* __restrict__ rowsum, int64_t nb,
                 int64_t R, int64_t C, int64_t Rp) {
   __shared__ int8_t tile[64][65];
-  const int64_t b = blockIdx.z;
-  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  __shared__ int colsum[4][64];
+  const int64_t b = blockIdx.y;
+  const int c0 = blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int8_t* s = src + b * R * C;
-  for (int i = ty; i < 64; i += 4) {
-    int r = r0 + i, c = c0 + tx;
-    tile[i][tx] = (r < R && c < C) ? s[(int64_t)r * C + c] : (int8_t)0;
-  }
-  __syncthreads();
   int8_t* d = dst + b * C * Rp;
-  for (int i = ty; i < 64; i += 4) {
-    int c = c0 + i, r = r0 + tx;
-    if (c < C && r < Rp) d[(int64_t)c * Rp + r] = tile[tx][i];
-  }
-  if (rowsum && blockIdx.x == 0 && ty == 0) {
-    // one lane per output row c: sum over all R (reads src directly; R is small)
-    int c = c0 + tx;
-    if (c < C) {
-      int64_t acc = 0;
-      for (int64_t r = 0; r < R; ++r) acc += s[r * C + c];
-      rowsum[b * C + c] = acc;
+  int csum = 0;
+  for (int r0 = 0; r0 < Rp; r0 += 64) {
+    for (int i = ty; i < 64; i += 4) {
+      const int r = r0 + i, c = c0 + tx;
+      const int8_t val = (r < R && c < C) ? s[(int64_t)r * C + c] : (int8_t)0;
+      tile[i][tx] = val;
+      csum += val;
     }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {
+      const int c = c0 + i, r = r0 + tx;
+      if (c < C && r < Rp) d[(int64_t)c * Rp + r] = tile[tx][i];
+    }
+    __syncthreads();
+  }
+  if (rowsum) {
+    colsum[ty][tx] = csum;
+    __syncthreads();
+    if (ty == 0 && c0 + tx < C)
+      rowsum[b * C + c0 + tx] = (int64_t)colsum[0][tx] + colsum[1][tx] + colsum[2][tx] + colsum[3][tx];
   }
 }
 
@@ -312,8 +368,6 @@ static Epi make_epi(const nqk_epilogue* p) {
   e.zpa = p->zpa;
   e.zpb = p->zpb;
   e.kdim = p->kdim;
-  e.row = p->row;
-  e.col = p->col;
   e.group_cols = p->group_cols > 0 ? p->group_cols : 1;
   for (int g = 0; g < 3; ++g) {
     e.s_acc[g] = p->s_acc[g];
@@ -344,13 +398,17 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     return fail("nqk_qgemm_fused: operands must be 16-byte aligned");
   if (batch > 65535) return fail("nqk_qgemm_fused: batch > 65535");
   if (params->bit_width < 2 || params->bit_width > 8) return fail("nqk_qgemm_fused: int8 outputs need 2 <= bw <= 8");
+  if (M > (1 << 30) || N > (1 << 30) || K > (1 << 30) || lda > (1 << 30) || ldb > (1 << 30))
+    return fail("nqk_qgemm_fused: dimensions beyond int32");
+  if (params->zp_flags & (NQK_ZP_SCALAR | NQK_ZP_FULL))
+    return fail("nqk_qgemm_fused: only row / column / K-constant zero-point terms");
   const int tiles_m = (int)((M + FBM - 1) / FBM), tiles_n = (int)((N + FBN - 1) / FBN);
   const BatchMap m = batch_map(bmap);
   const Epi e = make_epi(params);
   const dim3 grid(tiles_m * tiles_n, 1, (unsigned)batch);
   switch (epi) {
-#define L(E) case E: hipLaunchKernelGGL(k_qgemm_epi<E>, grid, dim3(256), 0, stream(), a, bt, M, N, K, lda, ldb, m, \
-                                        a_mat_stride, b_mat_stride, tiles_m, tiles_n, e); break;
+#define L(E) case E: hipLaunchKernelGGL(k_qgemm_epi<E>, grid, dim3(256), 0, stream(), a, bt, (int)M, (int)N, (int)K, \
+                                        (int)lda, (int)ldb, m, a_mat_stride, b_mat_stride, tiles_m, tiles_n, e); break;
     L(EPI_QKV) L(EPI_SCORES) L(EPI_PV) L(EPI_RESID) L(EPI_GELU)
 #undef L
     default: return fail("nqk_qgemm_fused: unknown epilogue");
@@ -364,8 +422,10 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
   PwPlan p;
   if (row_plan(cols, p)) return -1;
   const double lo = -__builtin_ldexp(1.0, bit_width - 1), hi = __builtin_ldexp(1.0, bit_width - 1) - 1.0;
-  hipLaunchKernelGGL(k_ln_quant, dim3(row_grid(rows)), dim3(64), row_smem(cols), stream(), x, gamma, beta, out, rows,
-                     cols, eps, p, scale, (double)zp, lo, hi);
+  const int64_t slice = (int64_t)(row_smem(cols) / sizeof(float) + 3) / 4 * 4;
+  const unsigned grid = (unsigned)(((rows + 3) / 4) < 65536 * 4 ? (rows + 3) / 4 : 65536 * 4);
+  hipLaunchKernelGGL(k_ln_quant, dim3(grid), dim3(256), 4 * slice * sizeof(float), stream(), x, gamma, beta, out,
+                     rows, cols, eps, p, scale, (double)zp, lo, hi, slice);
   return launch_status("nqk_ln_quant");
 }
 
@@ -376,8 +436,10 @@ extern "C" int nqk_softmax_quant(const float* x, int8_t* out, int64_t* rowsum, i
   PwPlan p;
   if (row_plan(cols, p)) return -1;
   const double lo = -__builtin_ldexp(1.0, bit_width - 1), hi = __builtin_ldexp(1.0, bit_width - 1) - 1.0;
-  hipLaunchKernelGGL(k_softmax_quant, dim3(row_grid(rows)), dim3(64), row_smem(cols), stream(), x, out, rowsum, rows,
-                     cols, ldo, p, scale, (double)zp, lo, hi);
+  const int64_t slice = (int64_t)(row_smem(cols) / sizeof(float) + 3) / 4 * 4;
+  const unsigned grid = (unsigned)(((rows + 3) / 4) < 65536 * 4 ? (rows + 3) / 4 : 65536 * 4);
+  hipLaunchKernelGGL(k_softmax_quant, dim3(grid), dim3(256), 4 * slice * sizeof(float), stream(), x, out, rowsum,
+                     rows, cols, ldo, p, scale, (double)zp, lo, hi, slice);
   return launch_status("nqk_softmax_quant");
 }
 
@@ -385,7 +447,7 @@ extern "C" int nqk_transpose_pad_i8(const int8_t* src, int8_t* dst, int64_t* row
                                     int64_t C, int64_t Rp) {
   if (nb <= 0 || R <= 0 || C <= 0) return 0;
   if (Rp < R || nb > 65535) return fail("nqk_transpose_pad_i8: bad shape");
-  const dim3 grid((unsigned)((Rp + 63) / 64), (unsigned)((C + 63) / 64), (unsigned)nb);
+  const dim3 grid((unsigned)((C + 63) / 64), (unsigned)nb, 1);
   hipLaunchKernelGGL(k_transpose_pad, grid, dim3(256), 0, stream(), src, dst, rowsum, nb, R, C, Rp);
   return launch_status("nqk_transpose_pad_i8");
 }

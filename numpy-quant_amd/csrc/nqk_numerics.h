@@ -54,7 +54,7 @@ __device__ __forceinline__ float ref_erf(float x) {
 // flattens it into leaves + a post-order combine program shared by every row.
 constexpr int kMaxLeaves = 64;
 struct PwPlan {
-  int nleaf, nops;
+  int nleaf, nops, balanced;  // balanced: nleaf = 2^k and a complete binary combine tree
   int start[kMaxLeaves], len[kMaxLeaves];
   signed char ops[2 * kMaxLeaves];  // >= 0: push leaf; -1: pop b, pop a, push a + b
 };
@@ -120,10 +120,85 @@ __device__ float row_pairwise_sum(const float* v, const PwPlan& p, float* part, 
   return t;
 }
 
+// wave-local LDS visibility: this wave's LDS writes are complete and ordered before
+// its later LDS reads (all lanes of a wave execute in lock step)
+__device__ __forceinline__ void wave_lds_sync() {
+  __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// NumPy pairwise sum of v[0..n) by ONE wave (any number of waves per block, each
+// with its own v / part / leafv regions; no block barrier).  part: 8*kMaxLeaves,
+// leafv: kMaxLeaves + 4 floats.
+__device__ float wave_pairwise_sum(const float* v, const PwPlan& p, float* part, float* leafv) {
+  const int lane = threadIdx.x & 63;
+  for (int c = lane; c < p.nleaf * 8; c += 64) {
+    const int l = c >> 3, j = c & 7;
+    const int L = p.len[l], s = p.start[l];
+    float r = 0.0f;
+    if (L >= 8) {
+      r = v[s + j];
+      const int end = L - (L % 8);
+      for (int i = 8 + j; i < end; i += 8) r = r + v[s + i];
+    }
+    part[c] = r;
+  }
+  wave_lds_sync();
+  for (int l = lane; l < p.nleaf; l += 64) {
+    const int L = p.len[l], s = p.start[l];
+    float res;
+    if (L < 8) {
+      res = 0.0f;
+      for (int i = 0; i < L; ++i) res = res + v[s + i];
+    } else {
+      const float* r = part + l * 8;
+      res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+      for (int i = L - (L % 8); i < L; ++i) res = res + v[s + i];
+    }
+    leafv[l] = res;
+  }
+  wave_lds_sync();
+  if (p.balanced) {
+    for (int cnt = p.nleaf; cnt > 1; cnt >>= 1) {
+      const int h = cnt >> 1;
+      float val = 0.0f;
+      if (lane < h) val = leafv[2 * lane] + leafv[2 * lane + 1];
+      wave_lds_sync();
+      if (lane < h) leafv[lane] = val;
+      wave_lds_sync();
+    }
+  } else if (lane == 0) {
+    float* st = part;  // the partials are consumed: reuse as the combine stack
+    int sp = 0;
+    for (int o = 0; o < p.nops; ++o) {
+      const int op = p.ops[o];
+      if (op >= 0) st[sp++] = leafv[op];
+      else { const float b = st[--sp]; const float a = st[--sp]; st[sp++] = a + b; }
+    }
+    leafv[0] = st[0];
+  }
+  wave_lds_sync();
+  const float t = leafv[0];
+  wave_lds_sync();
+  return t;
+}
+
 int row_plan(int64_t cols, PwPlan& p) {
   p.nleaf = 0;
   p.nops = 0;
+  p.balanced = 0;
   if (cols <= 0 || build_plan(cols, 0, p)) return fail("row length not supported by the pairwise-sum plan (max 8192)");
+  // balanced iff the post-order equals that of a complete tree over nleaf = 2^k leaves
+  if ((p.nleaf & (p.nleaf - 1)) == 0) {
+    signed char ref[2 * kMaxLeaves];
+    int n = 0, leaf = 0;
+    struct R { static void go(int cnt, signed char* ref, int& n, int& leaf) {
+      if (cnt == 1) { ref[n++] = (signed char)leaf++; return; }
+      go(cnt / 2, ref, n, leaf); go(cnt / 2, ref, n, leaf); ref[n++] = -1; } };
+    R::go(p.nleaf, ref, n, leaf);
+    p.balanced = (n == p.nops);
+    for (int k = 0; k < n && p.balanced; ++k) p.balanced = (ref[k] == p.ops[k]);
+  }
   return 0;
 }
 

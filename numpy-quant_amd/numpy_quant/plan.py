@@ -309,34 +309,30 @@ class FusedLayer:
              _f32(self.p_ln1.scale), _zp(self.p_ln1), bw)
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), col=self.col_qkv.ptr, group_cols=D,
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D,
                       s_acc=[_f32(s_a * np.float32(self.s_w[r])) for r in "qkv"],
                       s_out=[_f32(self.p_head[r].scale) for r in "qkv"],
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
                       out=[w["q"].ptr, w["k"].ptr, w["v"].ptr], bias=self.bias_qkv.ptr)
         _gemm(EPI_QKV, w["lnq"], self.bt_qkv, 1, Mrows, 3 * D, D, D, D, None, 0, 0, e)
-        # 3) zero-point row / column sums of the attention operands
-        call("nqk_rowsum", w["q"].vp, _lib.NQK_I8, w["qrs"].vp, 1, B * H * T, Dh, Dh, 0)
-        call("nqk_rowsum", w["k"].vp, _lib.NQK_I8, w["krs"].vp, 1, B * H * T, Dh, Dh, 0)
-        call("nqk_transpose_pad_i8", w["v"].vp, w["vt"].vp, w["vcs"].vp, B * H, T, Dh, Tp)
+        # 3) V -> V^T (the PV GEMM's Bt operand), zero padded to Tp tokens
+        call("nqk_transpose_pad_i8", w["v"].vp, w["vt"].vp, None, B * H, T, Dh, Tp)
         # 4) scores = dequant(Q K^T) / 8
         pq, pk, pv_ = self.p_head["q"], self.p_head["k"], self.p_head["v"]
         e = self._epi(zp_flags=_lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST, zpa=_zp(pq), zpb=_zp(pk), kdim=Dh,
-                      row=w["qrs"].ptr, col=w["krs"].ptr,
                       s_acc=[_f32(np.float32(pq.scale) * np.float32(pk.scale))], out=[w["s"].ptr], div=m.div)
         _gemm(EPI_SCORES, w["q"], w["k"], B * H, T, T, Dh, Dh, Dh, None, T * Dh, T * Dh, e)
         # 5) softmax + quantize (+ row sums for the PV zero-point term)
-        call("nqk_softmax_quant", w["s"].vp, w["p"].vp, w["prs"].vp, B * H * T, T, Tp,
+        call("nqk_softmax_quant", w["s"].vp, w["p"].vp, None, B * H * T, T, Tp,
              _f32(self.p_sm.scale), _zp(self.p_sm), bw)
         # 6) context = dequant(P V) -> Transpose -> Reshape -> quantize
         e = self._epi(zp_flags=_lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST, zpa=_zp(self.p_sm), zpb=_zp(pv_), kdim=T,
-                      row=w["prs"].ptr, col=w["vcs"].ptr,
                       s_acc=[_f32(np.float32(self.p_sm.scale) * np.float32(pv_.scale))],
                       s_out=[_f32(self.p_ctx.scale)], zp_out=[_zp(self.p_ctx)], out=[w["ctx"].ptr], ld_out=D)
         _gemm(EPI_PV, w["p"], w["vt"], B * H, T, Dh, Tp, Tp, Tp, None, T * Tp, Dh * Tp, e)
         # 7) output projection + bias + residual
         x1 = DeviceArray((B, T, D), np.float32)
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr,
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx),
                       s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
                       resid=x.dev.ptr, out=[x1.ptr])
         _gemm(EPI_RESID, w["ctx"], self.bt_o, 1, Mrows, D, D, D, D, None, 0, 0, e)
@@ -344,14 +340,14 @@ class FusedLayer:
         call("nqk_ln_quant", x1.vp, self.g2.vp, self.be2.vp, w["ln2q"].vp, Mrows, D, self.eps2,
              _f32(self.p_ln2.scale), _zp(self.p_ln2), bw)
         # 9) FFN up + bias + GELU + quantize
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr,
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2),
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
                       s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[w["h"].ptr],
                       div=m.gelu_div, add1=m.gelu_add, mul2=m.gelu_mul)
         _gemm(EPI_GELU, w["ln2q"], self.bt_1, 1, Mrows, F, D, D, D, None, 0, 0, e)
         # 10) FFN down + bias + residual
         x2 = DeviceArray((B, T, D), np.float32)
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr,
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h),
                       s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
                       resid=x1.ptr, out=[x2.ptr])
         _gemm(EPI_RESID, w["h"], self.bt_2, 1, Mrows, D, F, F, F, None, 0, 0, e)
@@ -398,9 +394,7 @@ class Workspace:
                 "lnq": DeviceArray((M, D), np.int8), "ln2q": DeviceArray((M, D), np.int8),
                 "q": DeviceArray((B * H * T, Dh), np.int8), "k": DeviceArray((B * H * T, Dh), np.int8),
                 "v": DeviceArray((B * H * T, Dh), np.int8), "vt": DeviceArray((B * H, Dh, Tp), np.int8),
-                "qrs": DeviceArray((B * H * T,), np.int64), "krs": DeviceArray((B * H * T,), np.int64),
-                "vcs": DeviceArray((B * H * Dh,), np.int64), "s": DeviceArray((B * H, T, T), np.float32),
-                "p": DeviceArray((B * H, T, Tp), np.int8), "prs": DeviceArray((B * H * T,), np.int64),
+                "s": DeviceArray((B * H, T, T), np.float32), "p": DeviceArray((B * H, T, Tp), np.int8),
                 "ctx": DeviceArray((M, D), np.int8), "h": DeviceArray((M, F), np.int8),
             }
             self.key = key
