@@ -175,9 +175,9 @@ int nqk_where_f32(const int64_t* cond, const float* a, const float* b, float* ou
 enum nqk_epi { NQK_EPI_QKV = 0, NQK_EPI_SCORES = 1, NQK_EPI_PV = 2, NQK_EPI_RESID = 3, NQK_EPI_GELU = 4 };
 typedef struct nqk_epilogue {
   int32_t zp_flags, bit_width, group_cols, tokens, heads, hdim, ld_out, pad0;
-  int64_t zpa, zpb, kdim;              /* zero-point term: ROW / COL / KCONST flags; the */
-  const int64_t* row_unused;           /* row sums of A and Bt are computed in-kernel     */
-  const int64_t* col_unused;
+  int64_t zpa, zpb, kdim;              /* zero-point term: ROW / COL / KCONST flags; row  */
+  const int64_t* row;                  /* sums of A and Bt are computed in-kernel unless  */
+  const int64_t* col;                  /* `col` holds precomputed int64 column sums of B  */
   float s_acc[3];                       /* dequant scale s_a*s_b per column group       */
   float s_out[3];                       /* quantize scale of the consumer value         */
   int64_t zp_out[3];                    /* quantize zero point of the consumer value    */

@@ -47,6 +47,7 @@ struct Epi {
   // row sums of A and of Bt are accumulated inside the kernel from the staged tiles
   int zp_flags;
   int64_t zpa, zpb, kdim;
+  const int64_t* colsum; // precomputed column sums of B (constant weights), or null
   int group_cols;        // columns per output group (EPI_QKV), else >= N
   float s_acc[3];        // dequant scale per group
   const float* bias;     // dequantized bias [N] or null
@@ -67,6 +68,62 @@ __device__ __forceinline__ int sum16(v4i c) {
   s = __builtin_amdgcn_sdot4(c[1], 0x01010101, s, false);
   s = __builtin_amdgcn_sdot4(c[2], 0x01010101, s, false);
   return __builtin_amdgcn_sdot4(c[3], 0x01010101, s, false);
+}
+
+// ---------------------------------------------------------------- shared epilogue
+struct EpiCol {
+  int64_t colterm;  // col-sum term minus the K constant
+  float bias;
+  int gn, g, hh, dd;
+  bool valid;
+};
+
+template <int EPI>
+__device__ __forceinline__ EpiCol epi_col(const Epi& e, int gn, int N, int64_t colsum_b, int64_t kconst) {
+  EpiCol c;
+  c.valid = gn < N;
+  c.gn = gn;
+  c.colterm = ((e.zp_flags & NQK_ZP_COL) ? colsum_b * e.zpa : 0) - kconst;
+  c.bias = (e.bias != nullptr && c.valid) ? e.bias[gn] : 0.0f;
+  c.g = 0;
+  c.hh = 0;
+  c.dd = gn;
+  if constexpr (EPI == EPI_QKV) {
+    c.g = gn / e.group_cols;
+    const int nloc = gn - c.g * e.group_cols;
+    c.hh = nloc / e.hdim;
+    c.dd = nloc - c.hh * e.hdim;
+  }
+  return c;
+}
+
+// one output element: v = acc - zpt -> dequant -> the consumer chain -> store
+template <int EPI>
+__device__ __forceinline__ void epi_elem(const Epi& e, int bz, int gm, int M, int N, int64_t rowterm, int img, int t,
+                                         int img_b, int head_b, const EpiCol& c, int32_t acc, float resid, bool ok) {
+  const int64_t v = (int64_t)acc - rowterm - c.colterm;
+  const int g = c.g;
+  const float d = (float)((double)v * (double)e.s_acc[g]);
+  const int gn = c.gn;
+  if constexpr (EPI == EPI_SCORES) {
+    const float y = d / e.div;
+    if (ok) ((float*)e.out[0])[((int64_t)bz * M + gm) * N + gn] = y;
+  } else if constexpr (EPI == EPI_RESID) {
+    const float y = (c.bias + d) + resid;
+    if (ok) ((float*)e.out[0])[(int64_t)gm * N + gn] = y;
+  } else if constexpr (EPI == EPI_GELU) {
+    const float h = c.bias + d;
+    const float a = ref_erf(h / e.div) + e.add1;
+    const float y = (h * a) * e.mul2;
+    const int q = quant_zp(y, e.s_out[0], e.zp_out[0], e.lo, e.hi);
+    if (ok) ((int8_t*)e.out[0])[(int64_t)gm * N + gn] = (int8_t)q;
+  } else if constexpr (EPI == EPI_QKV) {
+    const int q = quant_zp(c.bias + d, e.s_out[g], e.zp_out[g], e.lo, e.hi);
+    if (ok) ((int8_t*)e.out[g])[(((int64_t)img * e.heads + c.hh) * e.tokens + t) * e.hdim + c.dd] = (int8_t)q;
+  } else {  // EPI_PV
+    const int q = quant_zp(d, e.s_out[0], e.zp_out[0], e.lo, e.hi);
+    if (ok) ((int8_t*)e.out[0])[((int64_t)img_b * e.tokens + gm) * e.ld_out + head_b * e.hdim + gn] = (int8_t)q;
+  }
 }
 
 template <int EPI>
@@ -172,27 +229,11 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
 
   // ---------------- epilogue: per-column values hoisted, per-row values once per row
   const int64_t kconst = (e.zp_flags & NQK_ZP_KCONST) ? e.zpa * e.zpb * e.kdim : 0;
-  int64_t colterm[2];
-  float bias_j[2];
-  int gcol[2], grp[2], hh_j[2], dd_j[2];
-  bool nvalid[2];
+  EpiCol cols[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int nl = wn * 64 + j * 32 + r32;
-    const int gn = n0 + nl;
-    nvalid[j] = gn < N;
-    gcol[j] = gn;
-    colterm[j] = (need_rb ? (int64_t)rsB[nl] * e.zpa : 0) - kconst;
-    bias_j[j] = (e.bias != nullptr && nvalid[j]) ? e.bias[gn] : 0.0f;
-    grp[j] = 0;
-    hh_j[j] = 0;
-    dd_j[j] = gn;
-    if constexpr (EPI == EPI_QKV) {
-      grp[j] = gn / e.group_cols;
-      const int nloc = gn - grp[j] * e.group_cols;
-      hh_j[j] = nloc / e.hdim;
-      dd_j[j] = nloc - hh_j[j] * e.hdim;
-    }
+    cols[j] = epi_col<EPI>(e, n0 + nl, N, need_rb ? (int64_t)rsB[nl] : 0, kconst);
   }
   int img_b = 0, head_b = 0;
   if constexpr (EPI == EPI_PV) {
@@ -201,43 +242,173 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
+    float res[16][2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        res[r][j] = 0.0f;
+        if constexpr (EPI == EPI_RESID) {
+          const int gm = min(m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half, M - 1);
+          res[r][j] = e.resid[(int64_t)gm * N + min(cols[j].gn, N - 1)];
+        }
+      }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
       const int gm = m0 + ml;
-      if (gm >= M) continue;
-      const int64_t rowterm = need_ra ? (int64_t)rsA[ml] * e.zpb : 0;
+      const bool rok = gm < M;
+      const int64_t rowterm = need_ra ? (int64_t)rsA[min(ml, FBM - 1)] * e.zpb : 0;
       int img = 0, t = 0;
       if constexpr (EPI == EPI_QKV) {
         img = gm / e.tokens;
         t = gm - img * e.tokens;
       }
 #pragma unroll
+      for (int j = 0; j < 2; ++j)
+        epi_elem<EPI>(e, bz, gm, M, N, rowterm, img, t, img_b, head_b, cols[j], acc[i][j][r], res[r][j],
+                      rok && cols[j].valid);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Projection GEMM (A [M][K] activations x constant weights Bt [N][K]), batch 1:
+// 256x256 tiles, 8 waves (2 x 4, 128x64 each = 4x2 tiles of v_mfma_i32_32x32x32_i8),
+// BK = 64, a 4-stage LDS ring filled by global_load_lds_dwordx4 (no VGPR staging, 3 stages
+// in flight behind counted vmcnt waits), raw s_barrier.  The LDS image is lane-linear
+// per 1 KiB piece; the conflict-free chunk swizzle is applied to the SOURCE address.
+// Needs K % 64 == 0 and precomputed weight column sums (zero-point COL term only).
+constexpr int GBM = 256, GBN = 256, GBK = 64, GST = 4;
+constexpr int GSTAGE = (GBM + GBN) * GBK;  // 32 KiB
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+template <int N_OUT>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N_OUT == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N_OUT == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N_OUT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1)
+k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
+            int tiles_m, int tiles_n, Epi e) {
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  const int nwg = tiles_m * tiles_n;
+  int wg = blockIdx.x;
+  if (nwg >= 8) {
+    const int q = nwg / 8, r = nwg % 8, x = wg % 8;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
+  }
+  const int tm = wg / tiles_n, tn = wg % tiles_n;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // this lane's source rows / chunks for its two A and two B pieces (1 KiB = 16 rows each)
+  const int prow = lane >> 2, ppos = lane & 3;
+  const int8_t* asrc[2];
+  const int8_t* bsrc[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int row = (wave * 2 + p) * 16 + prow;
+    const int chunk = ppos ^ ((row >> 2) & 3);
+    const int am = min(m0 + row, M - 1), bn = min(n0 + row, N - 1);
+    asrc[p] = A + (int64_t)am * lda + chunk * 16;
+    bsrc[p] = Bt + (int64_t)bn * ldb + chunk * 16;
+  }
+  auto issue = [&](int st) {
+    int8_t* slot = lds + (st % GST) * GSTAGE;
+    const int k0 = st * GBK;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[p] + k0), (lds_ptr_t)(slot + (wave * 2 + p) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[p] + k0),
+                                       (lds_ptr_t)(slot + GBM * GBK + (wave * 2 + p) * 1024), 16, 0, 0);
+    }
+  };
+
+  v16i acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+
+  const int nk = K / GBK;
+#pragma unroll
+  for (int st = 0; st < GST - 1; ++st)
+    if (st < nk) issue(st);
+  const int r32 = lane & 31, half = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + GST - 1 < nk) issue(kt + GST - 1);
+    const int ahead = nk - 1 - kt;
+    if (ahead >= 3) wait_vmcnt<12>();
+    else if (ahead == 2) wait_vmcnt<8>();
+    else if (ahead == 1) wait_vmcnt<4>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int8_t* sa = lds + (kt % GST) * GSTAGE;
+    const int8_t* sb = sa + GBM * GBK;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      v4i fa[4], fb[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[i] = *reinterpret_cast<const v4i*>(sa + swz64(wm * 128 + i * 32 + r32, 2 * s + half));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * s + half));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  EpiCol cols[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int gn = n0 + wn * 64 + j * 32 + r32;
+    cols[j] = epi_col<EPI>(e, gn, N, (gn < N && e.colsum) ? e.colsum[gn] : 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float res[16][2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
       for (int j = 0; j < 2; ++j) {
-        if (!nvalid[j]) continue;
-        const int64_t v = (int64_t)acc[i][j][r] - rowterm - colterm[j];
-        const int g = grp[j];
-        const float d = (float)((double)v * (double)e.s_acc[g]);
-        const int gn = gcol[j];
-        if constexpr (EPI == EPI_SCORES) {
-          float* o = (float*)e.out[0];
-          o[((int64_t)bz * M + gm) * N + gn] = d / e.div;
-        } else if constexpr (EPI == EPI_RESID) {
-          const int64_t idx = (int64_t)gm * N + gn;
-          ((float*)e.out[0])[idx] = (bias_j[j] + d) + e.resid[idx];
-        } else if constexpr (EPI == EPI_GELU) {
-          const float h = bias_j[j] + d;
-          const float a = ref_erf(h / e.div) + e.add1;
-          const float y = (h * a) * e.mul2;
-          ((int8_t*)e.out[0])[(int64_t)gm * N + gn] = (int8_t)quant_zp(y, e.s_out[0], e.zp_out[0], e.lo, e.hi);
-        } else if constexpr (EPI == EPI_QKV) {
-          const int q = quant_zp(bias_j[j] + d, e.s_out[g], e.zp_out[g], e.lo, e.hi);
-          ((int8_t*)e.out[g])[(((int64_t)img * e.heads + hh_j[j]) * e.tokens + t) * e.hdim + dd_j[j]] = (int8_t)q;
-        } else {  // EPI_PV
-          const int q = quant_zp(d, e.s_out[0], e.zp_out[0], e.lo, e.hi);
-          ((int8_t*)e.out[0])[((int64_t)img_b * e.tokens + gm) * e.ld_out + head_b * e.hdim + gn] = (int8_t)q;
+        res[r][j] = 0.0f;
+        if constexpr (EPI == EPI_RESID) {
+          const int gm = min(m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half, M - 1);
+          res[r][j] = e.resid[(int64_t)gm * N + min(cols[j].gn, N - 1)];
         }
       }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int gm = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      const bool rok = gm < M;
+      int img = 0, t = 0;
+      if constexpr (EPI == EPI_QKV) {
+        img = gm / e.tokens;
+        t = gm - img * e.tokens;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        epi_elem<EPI>(e, 0, gm, M, N, 0, img, t, 0, 0, cols[j], acc[i][j][r], res[r][j], rok && cols[j].valid);
     }
   }
 }
@@ -368,6 +539,7 @@ static Epi make_epi(const nqk_epilogue* p) {
   e.zpa = p->zpa;
   e.zpb = p->zpb;
   e.kdim = p->kdim;
+  e.colsum = p->col;
   e.group_cols = p->group_cols > 0 ? p->group_cols : 1;
   for (int g = 0; g < 3; ++g) {
     e.s_acc[g] = p->s_acc[g];
@@ -402,9 +574,23 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     return fail("nqk_qgemm_fused: dimensions beyond int32");
   if (params->zp_flags & (NQK_ZP_SCALAR | NQK_ZP_FULL))
     return fail("nqk_qgemm_fused: only row / column / K-constant zero-point terms");
+  const Epi e = make_epi(params);
+  const bool big = batch == 1 && (K % GBK) == 0 && params->col != nullptr && params->zp_flags == NQK_ZP_COL &&
+                   (epi == EPI_QKV || epi == EPI_RESID || epi == EPI_GELU);
+  if (big) {
+    const int tm = (int)((M + GBM - 1) / GBM), tn = (int)((N + GBN - 1) / GBN);
+    const size_t shm = (size_t)GST * GSTAGE;
+    switch (epi) {
+#define LB(E) case E: hipLaunchKernelGGL(k_qgemm_big<E>, dim3(tm * tn), dim3(512), shm, stream(), a, bt, (int)M, \
+                                         (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break;
+      LB(EPI_QKV) LB(EPI_RESID) LB(EPI_GELU)
+#undef LB
+      default: break;
+    }
+    return launch_status("nqk_qgemm_fused(big)");
+  }
   const int tiles_m = (int)((M + FBM - 1) / FBM), tiles_n = (int)((N + FBN - 1) / FBN);
   const BatchMap m = batch_map(bmap);
-  const Epi e = make_epi(params);
   const dim3 grid(tiles_m * tiles_n, 1, (unsigned)batch);
   switch (epi) {
 #define L(E) case E: hipLaunchKernelGGL(k_qgemm_epi<E>, grid, dim3(256), 0, stream(), a, bt, (int)M, (int)N, (int)K, \

@@ -29,7 +29,7 @@ class Epilogue(ctypes.Structure):
                 ("tokens", ctypes.c_int32), ("heads", ctypes.c_int32), ("hdim", ctypes.c_int32),
                 ("ld_out", ctypes.c_int32), ("pad0", ctypes.c_int32),
                 ("zpa", ctypes.c_int64), ("zpb", ctypes.c_int64), ("kdim", ctypes.c_int64),
-                ("row_unused", ctypes.c_void_p), ("col_unused", ctypes.c_void_p),
+                ("row", ctypes.c_void_p), ("col", ctypes.c_void_p),
                 ("s_acc", ctypes.c_float * 3), ("s_out", ctypes.c_float * 3), ("zp_out", ctypes.c_int64 * 3),
                 ("out", ctypes.c_void_p * 3), ("bias", ctypes.c_void_p), ("resid", ctypes.c_void_p),
                 ("div", ctypes.c_float), ("add1", ctypes.c_float), ("mul2", ctypes.c_float),

@@ -309,7 +309,7 @@ class FusedLayer:
              _f32(self.p_ln1.scale), _zp(self.p_ln1), bw)
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D,
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D, col=self.col_qkv.ptr,
                       s_acc=[_f32(s_a * np.float32(self.s_w[r])) for r in "qkv"],
                       s_out=[_f32(self.p_head[r].scale) for r in "qkv"],
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
@@ -332,7 +332,7 @@ class FusedLayer:
         _gemm(EPI_PV, w["p"], w["vt"], B * H, T, Dh, Tp, Tp, Tp, None, T * Tp, Dh * Tp, e)
         # 7) output projection + bias + residual
         x1 = DeviceArray((B, T, D), np.float32)
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx),
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr,
                       s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
                       resid=x.dev.ptr, out=[x1.ptr])
         _gemm(EPI_RESID, w["ctx"], self.bt_o, 1, Mrows, D, D, D, D, None, 0, 0, e)
@@ -340,14 +340,14 @@ class FusedLayer:
         call("nqk_ln_quant", x1.vp, self.g2.vp, self.be2.vp, w["ln2q"].vp, Mrows, D, self.eps2,
              _f32(self.p_ln2.scale), _zp(self.p_ln2), bw)
         # 9) FFN up + bias + GELU + quantize
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2),
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr,
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
                       s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[w["h"].ptr],
                       div=m.gelu_div, add1=m.gelu_add, mul2=m.gelu_mul)
         _gemm(EPI_GELU, w["ln2q"], self.bt_1, 1, Mrows, F, D, D, D, None, 0, 0, e)
         # 10) FFN down + bias + residual
         x2 = DeviceArray((B, T, D), np.float32)
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h),
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr,
                       s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
                       resid=x1.ptr, out=[x2.ptr])
         _gemm(EPI_RESID, w["h"], self.bt_2, 1, Mrows, D, F, F, F, None, 0, 0, e)
