@@ -274,29 +274,25 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
 
 // ---------------------------------------------------------------------------------------
 // Projection GEMM (A [M][K] activations x constant weights Bt [N][K]), batch 1:
-// 256x256 tiles, 8 waves (2 x 4, 128x64 each = 4x2 tiles of v_mfma_i32_32x32x32_i8),
-// BK = 64, a 4-stage LDS ring filled by global_load_lds_dwordx4 (no VGPR staging, 3 stages
-// in flight behind counted vmcnt waits), raw s_barrier.  The LDS image is lane-linear
-// per 1 KiB piece; the conflict-free chunk swizzle is applied to the SOURCE address.
-// Needs K % 64 == 0 and precomputed weight column sums (zero-point COL term only).
-constexpr int GBM = 256, GBN = 256, GBK = 64, GST = 4;
-constexpr int GSTAGE = (GBM + GBN) * GBK;  // 32 KiB
+// 128x256 tiles, 4 waves (1 x 4, 128x64 each = 4x2 tiles of v_mfma_i32_32x32x32_i8),
+// BK = 64, a 3-stage LDS ring (72 KiB -> two blocks per CU, so one block's epilogue
+// overlaps the other's MFMA loop) filled by global_load_lds_dwordx4 behind counted
+// vmcnt waits and raw s_barriers.  The LDS image is lane-linear per 1 KiB piece; the
+// conflict-free chunk swizzle is applied to the SOURCE address.  Needs K % 64 == 0
+// and precomputed weight column sums (zero-point COL term only).
+constexpr int GBM = 128, GBN = 256, GBK = 64, GST = 3;
+constexpr int GSTAGE = (GBM + GBN) * GBK;  // 24 KiB
+constexpr int GAP = GBM * GBK / 1024 / 4;  // A pieces per wave per stage (2)
+constexpr int GBP = GBN * GBK / 1024 / 4;  // B pieces per wave per stage (4)
+constexpr int GPW = GAP + GBP;             // glds per wave per stage (6)
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int N_OUT>
-__device__ __forceinline__ void wait_vmcnt() {
-  if constexpr (N_OUT == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N_OUT == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N_OUT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-}
-
 template <int EPI>
-__global__ void __launch_bounds__(512, 1)
+__global__ void __launch_bounds__(256, 2)
 k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
             int tiles_m, int tiles_n, Epi e) {
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
@@ -309,29 +305,32 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   const int tm = wg / tiles_n, tn = wg % tiles_n;
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wn = wave;  // waves side by side along N
 
-  // this lane's source rows / chunks for its two A and two B pieces (1 KiB = 16 rows each)
+  // this lane's source row / chunk for each of its A and B pieces (1 KiB = 16 rows)
   const int prow = lane >> 2, ppos = lane & 3;
-  const int8_t* asrc[2];
-  const int8_t* bsrc[2];
+  const int8_t* asrc[GAP];
+  const int8_t* bsrc[GBP];
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int row = (wave * 2 + p) * 16 + prow;
-    const int chunk = ppos ^ ((row >> 2) & 3);
-    const int am = min(m0 + row, M - 1), bn = min(n0 + row, N - 1);
-    asrc[p] = A + (int64_t)am * lda + chunk * 16;
-    bsrc[p] = Bt + (int64_t)bn * ldb + chunk * 16;
+  for (int p = 0; p < GAP; ++p) {
+    const int row = (wave * GAP + p) * 16 + prow;
+    asrc[p] = A + (int64_t)min(m0 + row, M - 1) * lda + (ppos ^ ((row >> 2) & 3)) * 16;
+  }
+#pragma unroll
+  for (int p = 0; p < GBP; ++p) {
+    const int row = (wave * GBP + p) * 16 + prow;
+    bsrc[p] = Bt + (int64_t)min(n0 + row, N - 1) * ldb + (ppos ^ ((row >> 2) & 3)) * 16;
   }
   auto issue = [&](int st) {
     int8_t* slot = lds + (st % GST) * GSTAGE;
     const int k0 = st * GBK;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[p] + k0), (lds_ptr_t)(slot + (wave * 2 + p) * 1024), 16, 0, 0);
+    for (int p = 0; p < GAP; ++p)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[p] + k0), (lds_ptr_t)(slot + (wave * GAP + p) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < GBP; ++p)
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[p] + k0),
-                                       (lds_ptr_t)(slot + GBM * GBK + (wave * 2 + p) * 1024), 16, 0, 0);
-    }
+                                       (lds_ptr_t)(slot + GBM * GBK + (wave * GBP + p) * 1024), 16, 0, 0);
   };
 
   v16i acc[4][2];
@@ -348,12 +347,14 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     if (st < nk) issue(st);
   const int r32 = lane & 31, half = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + GST - 1 < nk) issue(kt + GST - 1);
-    const int ahead = nk - 1 - kt;
-    if (ahead >= 3) wait_vmcnt<12>();
-    else if (ahead == 2) wait_vmcnt<8>();
-    else if (ahead == 1) wait_vmcnt<4>();
-    else wait_vmcnt<0>();
+    if (kt + GST - 1 < nk) {
+      issue(kt + GST - 1);
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 stages after kt in flight
+    } else if (kt + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     const int8_t* sa = lds + (kt % GST) * GSTAGE;
@@ -362,8 +363,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     for (int s = 0; s < 2; ++s) {
       v4i fa[4], fb[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        fa[i] = *reinterpret_cast<const v4i*>(sa + swz64(wm * 128 + i * 32 + r32, 2 * s + half));
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const v4i*>(sa + swz64(i * 32 + r32, 2 * s + half));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         fb[j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * s + half));
@@ -393,13 +393,13 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
       for (int j = 0; j < 2; ++j) {
         res[r][j] = 0.0f;
         if constexpr (EPI == EPI_RESID) {
-          const int gm = min(m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half, M - 1);
+          const int gm = min(m0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half, M - 1);
           res[r][j] = e.resid[(int64_t)gm * N + min(cols[j].gn, N - 1)];
         }
       }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int gm = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      const int gm = m0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
       const bool rok = gm < M;
       int img = 0, t = 0;
       if constexpr (EPI == EPI_QKV) {
@@ -581,7 +581,7 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     const int tm = (int)((M + GBM - 1) / GBM), tn = (int)((N + GBN - 1) / GBN);
     const size_t shm = (size_t)GST * GSTAGE;
     switch (epi) {
-#define LB(E) case E: hipLaunchKernelGGL(k_qgemm_big<E>, dim3(tm * tn), dim3(512), shm, stream(), a, bt, (int)M, \
+#define LB(E) case E: hipLaunchKernelGGL(k_qgemm_big<E>, dim3(tm * tn), dim3(256), shm, stream(), a, bt, (int)M, \
                                          (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break;
       LB(EPI_QKV) LB(EPI_RESID) LB(EPI_GELU)
 #undef LB
