@@ -1,0 +1,78 @@
+#!/usr/bin/env python
+"""Per-kernel timing of the int8 GEMMs at the ViT-Base B=256 shapes (stream events,
+interleaved repetitions in one process).  Prints one line per (kernel, shape)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "numpy-quant_amd"))
+from numpy_quant import _lib  # noqa: E402
+from numpy_quant.device import DeviceArray  # noqa: E402
+
+_lib.ensure_init()
+M = int(os.environ.get("GM_M", 256 * 197))
+shapes = {"qkv": (2304, 768, 0), "out": (768, 768, 3), "up": (3072, 768, 4), "down": (768, 3072, 3)}
+rng = np.random.default_rng(0)
+
+
+def ev():
+    e = ctypes.c_void_p()
+    _lib.call("nqk_event_create", ctypes.byref(e))
+    return e
+
+
+def timeit(fn, reps=10):
+    a, b = ev(), ev()
+    fn()
+    _lib.call("nqk_event_record", a)
+    for _ in range(reps):
+        fn()
+    _lib.call("nqk_event_record", b)
+    ms = ctypes.c_float()
+    _lib.call("nqk_event_elapsed", a, b, ctypes.byref(ms))
+    return ms.value / reps
+
+
+A = {}
+for name, (N, K, epi) in shapes.items():
+    a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
+    bt = DeviceArray.from_host(rng.integers(-128, 128, size=(N, K), dtype=np.int8))
+    col = DeviceArray.from_host(np.zeros(N, np.int64))
+    bias = DeviceArray.from_host(np.zeros(N, np.float32))
+    resid = DeviceArray((M, N), np.float32)
+    out = DeviceArray((M, N), np.float32)
+    c32 = DeviceArray((M, N), np.int32)
+    outs = [DeviceArray((M, 768), np.int8) for _ in range(3)] if epi == 0 else [out]
+    e = _lib.Epilogue()
+    e.zp_flags = _lib.ZP_COL
+    e.bit_width = 8
+    e.group_cols = 768 if epi == 0 else (1 << 30)
+    e.tokens, e.heads, e.hdim = 197, 12, 64
+    e.zpa = 3
+    e.col = col.ptr
+    for g in range(3):
+        e.s_acc[g] = 1e-4
+        e.s_out[g] = 0.05
+        e.zp_out[g] = -3
+        e.out[g] = outs[min(g, len(outs) - 1)].ptr
+    if epi == 4:
+        h = DeviceArray((M, N), np.int8)
+        e.out[0] = h.ptr
+    e.bias = bias.ptr
+    e.resid = resid.ptr
+    e.div, e.add1, e.mul2 = 1.4142135, 1.0, 0.5
+    ops = 2.0 * M * N * K
+
+    def fused():
+        _lib.call("nqk_qgemm_fused", epi, a.vp, bt.vp, 1, M, N, K, K, K, None, 0, 0, ctypes.byref(e))
+
+    def plain():
+        _lib.call("nqk_qgemm_i8", a.vp, bt.vp, c32.vp, 1, M, N, K, K, K, N, None, 0, 0, 0)
+
+    for tag, fn in (("fused", fused), ("qgemm_i8", plain)):
+        ms = timeit(fn)
+        print(f"{name:5s} {tag:9s} M={M} N={N} K={K}: {ms * 1e3:8.1f} us  {ops / ms / 1e9:8.1f} TOPS  "
+              f"({100 * ops / ms / 1e9 / 5033.2:5.1f}% of int8 peak)", flush=True)
