@@ -34,10 +34,20 @@ __device__ __forceinline__ double qclip(double u, double lo, double hi) {
   return u > hi ? hi : u;
 }
 
-// quantize one f32 value with (s, zp) like numpy_quantization.py:24-34 (zp given)
-__device__ __forceinline__ int quant_zp(float x, float s, double zp, double lo, double hi) {
-  float t = x / s;
-  double u = zp + (double)t;
+// RN32(x / c) from the f64 reciprocal rc = RN64(1/c): bit-identical to the IEEE f32
+// division.  The quotient of two normal floats lies at least 2^-49 (relative) away
+// from every float32 rounding midpoint, while RN64(x * rc) is within 2^-52 of x/c, so
+// both round to the same float.  Results near the subnormal range take the division.
+__device__ __forceinline__ float div_rc(float x, float c, double rc) {
+  const float t = (float)((double)x * rc);
+  return __builtin_fabsf(t) < 0x1p-125f ? x / c : t;
+}
+
+// quantize one f32 value with (s, zp) like numpy_quantization.py:24-34 (zp given);
+// rs = RN64(1/s)
+__device__ __forceinline__ int quant_zp(float x, float s, double rs, double zp, double lo, double hi) {
+  const float t = div_rc(x, s, rs);
+  const double u = zp + (double)t;
   if (u != u) return (int)lo;  // unreachable for finite calibrated scales
   return (int)__builtin_rint(qclip(u, lo, hi));
 }
@@ -52,10 +62,12 @@ struct Epi {
   float s_acc[3];        // dequant scale per group
   const float* bias;     // dequantized bias [N] or null
   float s_out[3];        // quantize scale per group
+  double rs_out[3];      // RN64(1 / s_out)
   double zp_out[3];      // quantize zero point per group
   void* out[3];          // outputs per group
   const float* resid;    // residual [M][N]
   float div;             // EPI_SCORES divisor; EPI_GELU sqrt(2) constant
+  double rdiv;           // RN64(1 / div)
   float add1, mul2;      // EPI_GELU: + 1.0, * 0.5
   int tokens, heads, hdim, ld_out;
   double lo, hi;
@@ -72,7 +84,7 @@ __device__ __forceinline__ int sum16(v4i c) {
 
 // ---------------------------------------------------------------- shared epilogue
 struct EpiCol {
-  int64_t colterm;  // col-sum term minus the K constant
+  int64_t colterm;  // col-sum term minus the K constant (fits int32 when the kernel's I32 holds)
   float bias;
   int gn, g, hh, dd;
   bool valid;
@@ -98,35 +110,40 @@ __device__ __forceinline__ EpiCol epi_col(const Epi& e, int gn, int N, int64_t c
 }
 
 // one output element: v = acc - zpt -> dequant -> the consumer chain -> store
-template <int EPI>
+template <int EPI, bool I32>
 __device__ __forceinline__ void epi_elem(const Epi& e, int bz, int gm, int M, int N, int64_t rowterm, int img, int t,
                                          int img_b, int head_b, const EpiCol& c, int32_t acc, float resid, bool ok) {
-  const int64_t v = (int64_t)acc - rowterm - c.colterm;
+  double vd;
+  if constexpr (I32) {
+    vd = (double)(acc - (int32_t)rowterm - (int32_t)c.colterm);  // host-checked: no int32 overflow
+  } else {
+    vd = (double)((int64_t)acc - rowterm - c.colterm);
+  }
   const int g = c.g;
-  const float d = (float)((double)v * (double)e.s_acc[g]);
+  const float d = (float)(vd * (double)e.s_acc[g]);
   const int gn = c.gn;
   if constexpr (EPI == EPI_SCORES) {
-    const float y = d / e.div;
+    const float y = div_rc(d, e.div, e.rdiv);
     if (ok) ((float*)e.out[0])[((int64_t)bz * M + gm) * N + gn] = y;
   } else if constexpr (EPI == EPI_RESID) {
     const float y = (c.bias + d) + resid;
     if (ok) ((float*)e.out[0])[(int64_t)gm * N + gn] = y;
   } else if constexpr (EPI == EPI_GELU) {
     const float h = c.bias + d;
-    const float a = ref_erf(h / e.div) + e.add1;
+    const float a = ref_erf(div_rc(h, e.div, e.rdiv)) + e.add1;
     const float y = (h * a) * e.mul2;
-    const int q = quant_zp(y, e.s_out[0], e.zp_out[0], e.lo, e.hi);
+    const int q = quant_zp(y, e.s_out[0], e.rs_out[0], e.zp_out[0], e.lo, e.hi);
     if (ok) ((int8_t*)e.out[0])[(int64_t)gm * N + gn] = (int8_t)q;
   } else if constexpr (EPI == EPI_QKV) {
-    const int q = quant_zp(c.bias + d, e.s_out[g], e.zp_out[g], e.lo, e.hi);
+    const int q = quant_zp(c.bias + d, e.s_out[g], e.rs_out[g], e.zp_out[g], e.lo, e.hi);
     if (ok) ((int8_t*)e.out[g])[(((int64_t)img * e.heads + c.hh) * e.tokens + t) * e.hdim + c.dd] = (int8_t)q;
   } else {  // EPI_PV
-    const int q = quant_zp(d, e.s_out[0], e.zp_out[0], e.lo, e.hi);
+    const int q = quant_zp(d, e.s_out[0], e.rs_out[0], e.zp_out[0], e.lo, e.hi);
     if (ok) ((int8_t*)e.out[0])[((int64_t)img_b * e.tokens + gm) * e.ld_out + head_b * e.hdim + gn] = (int8_t)q;
   }
 }
 
-template <int EPI>
+template <int EPI, bool I32>
 __global__ void __launch_bounds__(256)
 k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
             BatchMap bm, int64_t a_ms, int64_t b_ms, int tiles_m, int tiles_n, Epi e) {
@@ -266,7 +283,7 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        epi_elem<EPI>(e, bz, gm, M, N, rowterm, img, t, img_b, head_b, cols[j], acc[i][j][r], res[r][j],
+        epi_elem<EPI, I32>(e, bz, gm, M, N, rowterm, img, t, img_b, head_b, cols[j], acc[i][j][r], res[r][j],
                       rok && cols[j].valid);
     }
   }
@@ -291,7 +308,7 @@ typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int EPI>
+template <int EPI, bool I32>
 __global__ void __launch_bounds__(256, 2)
 k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
             int tiles_m, int tiles_n, Epi e) {
@@ -408,7 +425,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        epi_elem<EPI>(e, 0, gm, M, N, 0, img, t, 0, 0, cols[j], acc[i][j][r], res[r][j], rok && cols[j].valid);
+        epi_elem<EPI, I32>(e, 0, gm, M, N, 0, img, t, 0, 0, cols[j], acc[i][j][r], res[r][j], rok && cols[j].valid);
     }
   }
 }
@@ -419,6 +436,7 @@ __global__ void __launch_bounds__(256)
 k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
            int8_t* __restrict__ out, int64_t rows, int64_t cols, float eps, PwPlan p, float s, double zp, double lo,
            double hi, int64_t slice) {
+  const double rs = 1.0 / (double)s;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float* v = sm + w * slice;
@@ -442,7 +460,7 @@ k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float
     for (int64_t i = lane; i < cols; i += 64) {
       const float d = xr[i] + nmean;
       const float y = ((d * inv) * g[i]) + b[i];
-      orow[i] = (int8_t)quant_zp(y, s, zp, lo, hi);
+      orow[i] = (int8_t)quant_zp(y, s, rs, zp, lo, hi);
     }
     wave_lds_sync();
   }
@@ -453,6 +471,7 @@ k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float
 __global__ void __launch_bounds__(256)
 k_softmax_quant(const float* __restrict__ x, int8_t* __restrict__ out, int64_t* __restrict__ rowsum, int64_t rows,
                 int64_t cols, int64_t ldo, PwPlan p, float s, double zp, double lo, double hi, int64_t slice) {
+  const double rs = 1.0 / (double)s;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float* v = sm + w * slice;
@@ -474,12 +493,13 @@ k_softmax_quant(const float* __restrict__ x, int8_t* __restrict__ out, int64_t* 
     for (int64_t i = lane; i < cols; i += 64) v[i] = np_expf(v[i] + nm);
     wave_lds_sync();
     const float ssum = wave_pairwise_sum(v, p, part, leafv);
+    const double rsum = 1.0 / (double)ssum;
     int8_t* orow = out + r * ldo;
     int64_t acc = 0;
     for (int64_t i = lane; i < ldo; i += 64) {
       int q = 0;
       if (i < cols) {
-        q = quant_zp(v[i] / ssum, s, zp, lo, hi);
+        q = quant_zp(div_rc(v[i], ssum, rsum), s, rs, zp, lo, hi);
         acc += q;
       }
       orow[i] = (int8_t)q;
@@ -544,12 +564,14 @@ static Epi make_epi(const nqk_epilogue* p) {
   for (int g = 0; g < 3; ++g) {
     e.s_acc[g] = p->s_acc[g];
     e.s_out[g] = p->s_out[g];
+    e.rs_out[g] = 1.0 / (double)p->s_out[g];
     e.zp_out[g] = (double)p->zp_out[g];
     e.out[g] = p->out[g];
   }
   e.bias = p->bias;
   e.resid = p->resid;
   e.div = p->div;
+  e.rdiv = 1.0 / (double)p->div;
   e.add1 = p->add1;
   e.mul2 = p->mul2;
   e.tokens = p->tokens;
@@ -575,14 +597,22 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   if (params->zp_flags & (NQK_ZP_SCALAR | NQK_ZP_FULL))
     return fail("nqk_qgemm_fused: only row / column / K-constant zero-point terms");
   const Epi e = make_epi(params);
+  // int32 zero-point algebra when |acc| + |row term| + |col term| + |K term| < 2^31
+  const double za = (double)(params->zpa < 0 ? -params->zpa : params->zpa);
+  const double zb = (double)(params->zpb < 0 ? -params->zpb : params->zpb);
+  const double kk = (double)(params->kdim > K ? params->kdim : K);
+  const double bound = 16384.0 * kk + 128.0 * kk * (za + zb) + za * zb * kk;
+  const bool i32 = bound < 2147483647.0 * 0.98;
   const bool big = batch == 1 && (K % GBK) == 0 && params->col != nullptr && params->zp_flags == NQK_ZP_COL &&
                    (epi == EPI_QKV || epi == EPI_RESID || epi == EPI_GELU);
   if (big) {
     const int tm = (int)((M + GBM - 1) / GBM), tn = (int)((N + GBN - 1) / GBN);
     const size_t shm = (size_t)GST * GSTAGE;
     switch (epi) {
-#define LB(E) case E: hipLaunchKernelGGL(k_qgemm_big<E>, dim3(tm * tn), dim3(256), shm, stream(), a, bt, (int)M, \
-                                         (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break;
+#define LB(E) case E: if (i32) hipLaunchKernelGGL((k_qgemm_big<E, true>), dim3(tm * tn), dim3(256), shm, stream(), a, bt, \
+                                  (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); \
+                       else hipLaunchKernelGGL((k_qgemm_big<E, false>), dim3(tm * tn), dim3(256), shm, stream(), a, bt, \
+                                  (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break;
       LB(EPI_QKV) LB(EPI_RESID) LB(EPI_GELU)
 #undef LB
       default: break;
@@ -593,8 +623,10 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   const BatchMap m = batch_map(bmap);
   const dim3 grid(tiles_m * tiles_n, 1, (unsigned)batch);
   switch (epi) {
-#define L(E) case E: hipLaunchKernelGGL(k_qgemm_epi<E>, grid, dim3(256), 0, stream(), a, bt, (int)M, (int)N, (int)K, \
-                                        (int)lda, (int)ldb, m, a_mat_stride, b_mat_stride, tiles_m, tiles_n, e); break;
+#define L(E) case E: if (i32) hipLaunchKernelGGL((k_qgemm_epi<E, true>), grid, dim3(256), 0, stream(), a, bt, (int)M, \
+                                 (int)N, (int)K, (int)lda, (int)ldb, m, a_mat_stride, b_mat_stride, tiles_m, tiles_n, e); \
+                      else hipLaunchKernelGGL((k_qgemm_epi<E, false>), grid, dim3(256), 0, stream(), a, bt, (int)M, \
+                                 (int)N, (int)K, (int)lda, (int)ldb, m, a_mat_stride, b_mat_stride, tiles_m, tiles_n, e); break;
     L(EPI_QKV) L(EPI_SCORES) L(EPI_PV) L(EPI_RESID) L(EPI_GELU)
 #undef L
     default: return fail("nqk_qgemm_fused: unknown epilogue");
