@@ -21,7 +21,6 @@ unique-id exchange, barriers and the max-over-ranks of the step time.
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -46,15 +45,23 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def build_qmodel(batch: int, bit_width: int, calib_batch: int = 8):
+def build_qmodel(batch: int, bit_width: int, group=None, calib_batch: int = 8):
+    """Model.from_onnx + calibration (rank 0 only, shared with every replica) + the
+    graph rewrite of Model.quantize, rebatched to `batch`."""
     from numpy_quant import onnx_proto
     from numpy_quant.model import Model
+    from numpy_quant.replicas import ReplicaGroup
+    group = group or ReplicaGroup(rank=0, world=1)
     proto = onnx_proto.load(MODEL_FILE, synthetic_weights=True)
     model = Model.from_onnx(proto)
     model.rebatch(calib_batch)
-    rng = np.random.default_rng(12345)
-    x_cal = rng.standard_normal((calib_batch, 3, 224, 224)).astype(np.float32)
-    vmin, vmax = model.calibrate([x_cal])
+
+    def calibrate():
+        rng = np.random.default_rng(12345)
+        x_cal = rng.standard_normal((calib_batch, 3, 224, 224)).astype(np.float32)
+        return model.calibrate([x_cal])
+
+    vmin, vmax = group.shared_calibration(calibrate)
     from numpy_quant.numpy_quantization import quant_parameters
     from numpy_quant.model import QuantizationParams
     qp_cache = {}
@@ -120,80 +127,48 @@ def main():
     ap.add_argument("--eager", action="store_true", help="node-by-node executor instead of the fused plan")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://")
-
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray, sync
+    from numpy_quant.replicas import ReplicaGroup
     from numpy_quant.tensor import FTensor
-    _lib.ensure_init(local_rank)
+    group = ReplicaGroup()
+    rank, world = group.rank, group.world
+    _lib.ensure_init(group.local_rank)
 
     t_setup = time.time()
-    model, qmodel = build_qmodel(args.batch, args.bit_width)
+    model, qmodel = build_qmodel(args.batch, args.bit_width, group)
+    if world > 1:
+        # rank 0's quantized constants are the single source of truth (before compile)
+        nbytes = group.broadcast_constants(qmodel)
+        log(f"[bench] RCCL broadcast of {nbytes / 1e6:.1f} MB quantized constants")
     if not args.eager:
         plan = qmodel.compile()
         log(f"[bench] fused plan: {plan.fused} encoder layers fused, {len(plan.steps)} steps")
     log(f"[bench] model built + calibrated in {time.time() - t_setup:.1f}s")
 
-    if world > 1:
-        # RCCL communicator: unique id from rank 0 over the gloo control plane
-        uid = (ctypes.c_char * 128)()
-        if rank == 0:
-            _lib.call("nqk_comm_unique_id", uid)
-        obj = [bytes(uid)] if rank == 0 else [None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = (ctypes.c_char * 128).from_buffer_copy(obj[0])
-        _lib.call("nqk_comm_init", uid, world, rank)
-        # one-time broadcast of the packed quantized weights (+ qparams via gloo)
-        nbytes = 0
-        for v in qmodel.values:
-            d = v.data
-            if v.__class__.__name__ == "Constant" and hasattr(d, "dev"):
-                _lib.call("nqk_comm_bcast", d.dev.vp, d.dev.nbytes, 0)
-                nbytes += d.dev.nbytes
-        sync()
-        log(f"[bench] RCCL broadcast of {nbytes / 1e6:.1f} MB packed weights")
-
     rng = np.random.default_rng(256 + rank)
     x = rng.standard_normal((args.batch, 3, 224, 224)).astype(np.float32)
     x_dev = FTensor(x)  # resident in HBM before timing
-    logits_all = None
-    if world > 1 and rank == 0:
-        logits_all = DeviceArray((world, args.batch, 1000), np.float32)
-    gbuf = DeviceArray((args.batch, 1000), np.float32) if (world > 1 and rank != 0) else None
+    logits_all = DeviceArray((world, args.batch, 1000), np.float32) if (world > 1 and rank == 0) else None
 
     def step():
         qmodel.set_inputs([x_dev])
         qmodel.run()
         out = qmodel.outputs_device()[0]
-        if world > 1:
-            _lib.call("nqk_comm_gather", out.dev.vp, logits_all.vp if rank == 0 else gbuf.vp,
-                      out.dev.nbytes, 0)
+        group.gather(out.dev, logits_all)
         return out
 
     for _ in range(args.warmup):
         step()
     sync()
-    if dist:
-        dist.barrier()
+    group.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     sync()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t[0])
+    group.barrier()
+    dt = group.max(time.perf_counter() - t0)
     ms_per_step = 1e3 * dt / args.steps
     samples = args.batch * world * args.steps
     value = samples / dt
@@ -230,9 +205,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args.bit_width)
         print(json.dumps(res), flush=True)
-    if world > 1:
-        _lib.call("nqk_comm_destroy")
-        dist.destroy_process_group()
+    group.close()
 
 
 if __name__ == "__main__":
