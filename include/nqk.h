@@ -172,7 +172,8 @@ int nqk_where_f32(const int64_t* cond, const float* a, const float* b, float* ou
 /* ------------------------------------------- fused device plan (plan.py) */
 /* Epilogue of nqk_qgemm_fused: the consumer chain of a q_matmul output as the
  * reference's node loop runs it (dequantize -> float ops -> quantize), per element. */
-enum nqk_epi { NQK_EPI_QKV = 0, NQK_EPI_SCORES = 1, NQK_EPI_PV = 2, NQK_EPI_RESID = 3, NQK_EPI_GELU = 4 };
+enum nqk_epi { NQK_EPI_QKV = 0, NQK_EPI_SCORES = 1, NQK_EPI_PV = 2, NQK_EPI_RESID = 3, NQK_EPI_GELU = 4,
+               NQK_EPI_NULL = 5 /* diagnostic: no stores (main-loop timing) */ };
 typedef struct nqk_epilogue {
   int32_t zp_flags, bit_width, group_cols, tokens, heads, hdim, ld_out, pad0;
   int64_t zpa, zpb, kdim;              /* zero-point term: ROW / COL / KCONST flags; row  */

@@ -72,7 +72,10 @@ for name, (N, K, epi) in shapes.items():
     def plain():
         _lib.call("nqk_qgemm_i8", a.vp, bt.vp, c32.vp, 1, M, N, K, K, K, N, None, 0, 0, 0)
 
-    for tag, fn in (("fused", fused), ("qgemm_i8", plain)):
+    def null():
+        _lib.call("nqk_qgemm_fused", 5, a.vp, bt.vp, 1, M, N, K, K, K, None, 0, 0, ctypes.byref(e))
+
+    for tag, fn in (("fused", fused), ("null_epi", null), ("qgemm_i8", plain)):
         ms = timeit(fn)
         print(f"{name:5s} {tag:9s} M={M} N={N} K={K}: {ms * 1e3:8.1f} us  {ops / ms / 1e9:8.1f} TOPS  "
               f"({100 * ops / ms / 1e9 / 5033.2:5.1f}% of int8 peak)", flush=True)
