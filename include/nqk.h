@@ -206,6 +206,24 @@ int nqk_softmax_quant(const float* x, int8_t* out, int64_t* rowsum, int64_t rows
 int nqk_transpose_pad_i8(const int8_t* src, int8_t* dst, int64_t* rowsum, int64_t nb, int64_t R, int64_t C,
                          int64_t Rp);
 
+/* Fused self-attention of one layer: MatMul(Q, K^T) -> Div -> Softmax -> quantize ->
+ * MatMul(P, V) -> Transpose -> Reshape -> quantize (model.py:153-157 MatMul, tensor.py:139-146
+ * softmax, numpy_quantization.py:24-61 quantize / q_matmul), bit-identical to
+ * nqk_qgemm_fused(SCORES) + nqk_softmax_quant + nqk_qgemm_fused(PV).
+ * q, k, v: int8 [batch_heads][tokens][64]; ctx: int8 [batch_heads / heads][tokens][ld_out],
+ * head h at columns h*64.  tokens <= 224; |zq|,|zk| <= 4096, |zp_p|,|zv| <= 1024. */
+typedef struct nqk_attention {
+  int32_t heads, tokens, hdim, ld_out, bit_width, pad0;
+  int64_t zq, zk;          /* zero points of the quantized Q and K^T                 */
+  float s_qk, div;         /* f32(s_q * s_k), the scores Div constant                */
+  float s_p, s_pv;         /* softmax-output scale, f32(s_p * s_v)                   */
+  int64_t zp_p, zv;        /* zero points of P and V                                 */
+  float s_ctx, pad1;       /* context quantization scale                             */
+  int64_t zp_ctx;          /* context zero point                                     */
+} nqk_attention;
+int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_t* v, int8_t* ctx, int64_t batch_heads,
+                        const nqk_attention* params);
+
 /* ------------------------------------------------ multi-GPU replicas (RCCL) */
 int nqk_comm_unique_id(void* id128);                         /* rank 0 */
 int nqk_comm_init(const void* id128, int nranks, int rank);

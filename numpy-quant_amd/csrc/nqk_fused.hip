@@ -145,6 +145,104 @@ __device__ __forceinline__ void epi_elem(const Epi& e, int bz, int gm, int M, in
   }
 }
 
+// ---------------------------------------------------------------- 4-column epilogue
+// (row-major staged tiles: one lane, one row, 4 consecutive columns of one head/group)
+struct EpiCol4 {
+  int64_t colterm[4];
+  float bias[4];
+  float s_acc, s_out;  // per-lane copies of the column group's scalars (no dynamic
+  double rs_out, zp;   // indexing into the kernel-argument struct inside the row loop)
+  int8_t* out;
+  int hh, dd;
+};
+
+template <int EPI>
+__device__ __forceinline__ EpiCol4 epi_col4(const Epi& e, int gn0, bool ok) {
+  EpiCol4 c;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    c.colterm[k] = (ok && (e.zp_flags & NQK_ZP_COL)) ? e.colsum[gn0 + k] * e.zpa : 0;
+    c.bias[k] = (ok && e.bias != nullptr) ? e.bias[gn0 + k] : 0.0f;
+  }
+  int g = 0;
+  c.hh = 0;
+  c.dd = gn0;
+  if constexpr (EPI == EPI_QKV) {
+    g = gn0 / e.group_cols;
+    const int nloc = gn0 - g * e.group_cols;
+    c.hh = nloc / e.hdim;
+    c.dd = nloc - c.hh * e.hdim;
+  }
+  g = g > 2 ? 2 : g;
+  c.s_acc = g == 0 ? e.s_acc[0] : (g == 1 ? e.s_acc[1] : e.s_acc[2]);
+  c.s_out = g == 0 ? e.s_out[0] : (g == 1 ? e.s_out[1] : e.s_out[2]);
+  c.rs_out = g == 0 ? e.rs_out[0] : (g == 1 ? e.rs_out[1] : e.rs_out[2]);
+  c.zp = g == 0 ? e.zp_out[0] : (g == 1 ? e.zp_out[1] : e.zp_out[2]);
+  c.out = (int8_t*)(g == 0 ? e.out[0] : (g == 1 ? e.out[1] : e.out[2]));
+  return c;
+}
+
+// RN32(x / c) as div_rc, with the (exact) f32 division taken only in a wave-uniform
+// branch when some lane's quotient is near the subnormal range (never on these paths)
+__device__ __forceinline__ float div_rc_u(float x, float c, double rc) {
+  float t = (float)((double)x * rc);
+  const bool slow = __builtin_fabsf(t) < 0x1p-125f && x != 0.0f;
+  if (__builtin_expect(__any(slow), 0)) t = slow ? x / c : t;
+  return t;
+}
+
+// quantize (numpy_quantization.py:24-34) with max/min clipping: a NaN clips to lo, as
+// quant_zp returns; finite values are identical to the compare-based clip
+__device__ __forceinline__ int quant_zp_u(float x, float s, double rs, double zp, double lo, double hi) {
+  const float t = div_rc_u(x, s, rs);
+  const double u = zp + (double)t;
+  return (int)__builtin_rint(__builtin_fmin(__builtin_fmax(u, lo), hi));
+}
+
+template <int EPI, bool I32>
+__device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, int N, const EpiCol4& c, v4i a,
+                                         float4 r) {
+  float d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double vd;
+    if constexpr (I32) vd = (double)(a[k] - (int32_t)c.colterm[k]);
+    else vd = (double)((int64_t)a[k] - c.colterm[k]);
+    d[k] = (float)(vd * (double)c.s_acc);
+  }
+  if constexpr (EPI == EPI_RESID) {
+    const int64_t o = (int64_t)gm * N + c.dd;
+    float4 y;
+    y.x = (c.bias[0] + d[0]) + r.x;
+    y.y = (c.bias[1] + d[1]) + r.y;
+    y.z = (c.bias[2] + d[2]) + r.z;
+    y.w = (c.bias[3] + d[3]) + r.w;
+    *reinterpret_cast<float4*>((float*)e.out[0] + o) = y;
+  } else if constexpr (EPI == EPI_NULL) {
+    if (a[0] == (int32_t)0x80000001) ((int32_t*)e.out[0])[0] = (int)d[1];
+  } else {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int q;
+      if constexpr (EPI == EPI_GELU) {
+        const float h = c.bias[k] + d[k];
+        const float aa = ref_erf(div_rc_u(h, e.div, e.rdiv)) + e.add1;
+        const float y = (h * aa) * e.mul2;
+        q = quant_zp_u(y, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+      } else {  // EPI_QKV
+        q = quant_zp_u(c.bias[k] + d[k], c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+      }
+      packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+    }
+    if constexpr (EPI == EPI_GELU) {
+      *reinterpret_cast<uint32_t*>(c.out + (int64_t)gm * N + c.dd) = packed;
+    } else {
+      *reinterpret_cast<uint32_t*>(c.out + (((int64_t)img * e.heads + c.hh) * e.tokens + t) * e.hdim + c.dd) = packed;
+    }
+  }
+}
+
 template <int EPI, bool I32>
 __global__ void __launch_bounds__(256)
 k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
@@ -397,38 +495,59 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  EpiCol cols[2];
+  // ---- epilogue, staged through LDS (the ring is free after the last barrier): each
+  // wave owns a 64 x 72-int32 slice; two passes of 64 rows.  Read back row-major, a lane
+  // takes 4 consecutive columns of one row, so bias / column terms are per lane and the
+  // outputs leave as 4-byte (int8) or 16-byte (f32) stores.
+  int32_t* stg = reinterpret_cast<int32_t*>(lds) + wave * (64 * 72);
+  const int c4 = (lane & 15) * 4;
+  const int gn0 = n0 + wn * 64 + c4;
+  const bool cok = gn0 < N;  // N % 4 == 0 (host-checked): the 4 columns are valid together
+  EpiCol4 cc = epi_col4<EPI>(e, gn0, cok);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int gn = n0 + wn * 64 + j * 32 + r32;
-    cols[j] = epi_col<EPI>(e, gn, N, (gn < N && e.colsum) ? e.colsum[gn] : 0, 0);
-  }
+  for (int pass = 0; pass < 2; ++pass) {
+    // residual rows of this pass in flight while the tile is staged
+    float4 rv[16];
+    if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float res[16][2];
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        res[r][j] = 0.0f;
-        if constexpr (EPI == EPI_RESID) {
-          const int gm = min(m0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half, M - 1);
-          res[r][j] = e.resid[(int64_t)gm * N + min(cols[j].gn, N - 1)];
-        }
+      for (int it = 0; it < 16; ++it) {
+        const int gm = min(m0 + pass * 64 + it * 4 + (lane >> 4), M - 1);
+        rv[it] = cok ? *reinterpret_cast<const float4*>(e.resid + (int64_t)gm * N + gn0) : make_float4(0, 0, 0, 0);
       }
+    }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int gm = m0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      const bool rok = gm < M;
-      int img = 0, t = 0;
-      if constexpr (EPI == EPI_QKV) {
-        img = gm / e.tokens;
-        t = gm - img * e.tokens;
-      }
+    for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        epi_elem<EPI, I32>(e, 0, gm, M, N, 0, img, t, 0, 0, cols[j], acc[i][j][r], res[r][j], rok && cols[j].valid);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          stg[(ii * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 72 + j * 32 + r32] = acc[2 * pass + ii][j][r];
+    wave_lds_sync();
+    // image / token of this lane's row, advanced incrementally (4 rows per step)
+    int gm = m0 + pass * 64 + (lane >> 4);
+    int img = 0, t = 0;
+    if constexpr (EPI == EPI_QKV) {
+      img = gm / e.tokens;
+      t = gm - img * e.tokens;
     }
+    auto row_step = [&](int it, float4 r4) {
+      const int rl = it * 4 + (lane >> 4);
+      const v4i a4 = *reinterpret_cast<const v4i*>(stg + rl * 72 + c4);
+      if (gm < M && cok) epi_row4<EPI, I32>(e, gm, img, t, N, cc, a4, r4);
+      gm += 4;
+      if constexpr (EPI == EPI_QKV) {
+        t += 4;
+        while (t >= e.tokens) { t -= e.tokens; ++img; }
+      }
+    };
+    if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) row_step(it, rv[it]);
+    } else {
+#pragma unroll 2
+      for (int it = 0; it < 16; ++it) row_step(it, make_float4(0, 0, 0, 0));
+    }
+    wave_lds_sync();
   }
 }
 
@@ -605,9 +724,14 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   const double kk = (double)(params->kdim > K ? params->kdim : K);
   const double bound = 16384.0 * kk + 128.0 * kk * (za + zb) + za * zb * kk;
   const bool i32 = bound < 2147483647.0 * 0.98;
-  const bool big = batch == 1 && (K % GBK) == 0 && params->col != nullptr && params->zp_flags == NQK_ZP_COL &&
+  const bool big = batch == 1 && (K % GBK) == 0 && (N % 4) == 0 && params->zp_flags == NQK_ZP_COL &&
+                   params->col != nullptr && (epi != EPI_QKV || (params->hdim % 4 == 0 && params->group_cols % 4 == 0)) &&
                    (epi == EPI_QKV || epi == EPI_RESID || epi == EPI_GELU || epi == EPI_NULL);
-  if (big) {
+  // staged epilogue stores 4 columns at once: 16-byte (f32) / 4-byte (int8) aligned outputs
+  auto al = [](const void* q, uintptr_t n) { return q == nullptr || (((uintptr_t)q) & (n - 1)) == 0; };
+  const bool aligned = (epi == EPI_RESID) ? (al(params->out[0], 16) && al(params->resid, 16))
+                                          : (al(params->out[0], 4) && al(params->out[1], 4) && al(params->out[2], 4));
+  if (big && aligned) {
     const int tm = (int)((M + GBM - 1) / GBM), tn = (int)((N + GBN - 1) / GBN);
     const size_t shm = (size_t)GST * GSTAGE;
     switch (epi) {

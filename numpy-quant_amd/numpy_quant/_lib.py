@@ -36,6 +36,16 @@ class Epilogue(ctypes.Structure):
                 ("pad1", ctypes.c_float)]
 
 
+class Attention(ctypes.Structure):
+    """Mirror of `nqk_attention` (include/nqk.h)."""
+    _fields_ = [("heads", ctypes.c_int32), ("tokens", ctypes.c_int32), ("hdim", ctypes.c_int32),
+                ("ld_out", ctypes.c_int32), ("bit_width", ctypes.c_int32), ("pad0", ctypes.c_int32),
+                ("zq", ctypes.c_int64), ("zk", ctypes.c_int64),
+                ("s_qk", ctypes.c_float), ("div", ctypes.c_float), ("s_p", ctypes.c_float), ("s_pv", ctypes.c_float),
+                ("zp_p", ctypes.c_int64), ("zv", ctypes.c_int64),
+                ("s_ctx", ctypes.c_float), ("pad1", ctypes.c_float), ("zp_ctx", ctypes.c_int64)]
+
+
 SIGNATURES = {
     "nqk_init": [_i],
     "nqk_device_count": [ctypes.POINTER(_i)],
@@ -79,6 +89,7 @@ SIGNATURES = {
     "nqk_ln_quant": [_p, _p, _p, _p, _l, _l, _f, _f, _l, _i],
     "nqk_softmax_quant": [_p, _p, _p, _l, _l, _l, _f, _l, _i],
     "nqk_transpose_pad_i8": [_p, _p, _p, _l, _l, _l, _l],
+    "nqk_attention_fused": [_p, _p, _p, _p, _l, _p],
     "nqk_comm_unique_id": [_p],
     "nqk_comm_init": [_p, _i, _i],
     "nqk_comm_bcast": [_p, ctypes.c_size_t, _i],

@@ -27,6 +27,9 @@ from .tensor import FTensor, QTensor
 
 EPI_QKV, EPI_SCORES, EPI_PV, EPI_RESID, EPI_GELU = 0, 1, 2, 3, 4
 
+# module switch: the one-kernel attention (nqk_attention_fused) where it applies
+FUSED_ATTENTION = True
+
 
 Epilogue = _lib.Epilogue
 
@@ -275,6 +278,11 @@ class FusedLayer:
         self.F = self.bt_1.shape[0]
         if self.D != m.heads * m.hdim or self.bt_o.shape != (self.D, self.D) or self.bt_2.shape != (self.D, self.F):
             raise NoMatch("layer dimensions")
+        # the one-kernel attention covers head size 64, <= 224 tokens and zero points for
+        # which every int32 intermediate is exact (nqk.h); otherwise three launches
+        zs = [_zp(self.p_head["q"]), _zp(self.p_head["k"]), _zp(self.p_sm), _zp(self.p_head["v"])]
+        self.attn_fused = (FUSED_ATTENTION and m.hdim == 64 and 1 <= m.tokens <= 224 and
+                           abs(zs[0]) <= 4096 and abs(zs[1]) <= 4096 and abs(zs[2]) <= 1024 and abs(zs[3]) <= 1024)
 
     def _epi(self, **kw) -> Epilogue:
         e = Epilogue()
@@ -291,6 +299,25 @@ class FusedLayer:
                 setattr(e, k, v)
         return e
 
+    def _attention_unfused(self, w, B, T, Tp, H, Dh, D):
+        """Scores GEMM, softmax and PV GEMM as three launches (any T / head size)."""
+        m, bw, call = self.m, self.bw, _lib.call
+        pq, pk, pv_ = self.p_head["q"], self.p_head["k"], self.p_head["v"]
+        # V -> V^T (the PV GEMM's Bt operand), zero padded to Tp tokens
+        call("nqk_transpose_pad_i8", w["v"].vp, w["vt"].vp, None, B * H, T, Dh, Tp)
+        # scores = dequant(Q K^T) / div
+        e = self._epi(zp_flags=_lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST, zpa=_zp(pq), zpb=_zp(pk), kdim=Dh,
+                      s_acc=[_f32(np.float32(pq.scale) * np.float32(pk.scale))], out=[w["s"].ptr], div=m.div)
+        _gemm(EPI_SCORES, w["q"], w["k"], B * H, T, T, Dh, Dh, Dh, None, T * Dh, T * Dh, e)
+        # softmax + quantize
+        call("nqk_softmax_quant", w["s"].vp, w["p"].vp, None, B * H * T, T, Tp,
+             _f32(self.p_sm.scale), _zp(self.p_sm), bw)
+        # context = dequant(P V) -> Transpose -> Reshape -> quantize
+        e = self._epi(zp_flags=_lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST, zpa=_zp(self.p_sm), zpb=_zp(pv_), kdim=T,
+                      s_acc=[_f32(np.float32(self.p_sm.scale) * np.float32(pv_.scale))],
+                      s_out=[_f32(self.p_ctx.scale)], zp_out=[_zp(self.p_ctx)], out=[w["ctx"].ptr], ld_out=D)
+        _gemm(EPI_PV, w["p"], w["vt"], B * H, T, Dh, Tp, Tp, Tp, None, T * Tp, Dh * Tp, e)
+
     def run(self, ws: "Workspace"):
         m, bw = self.m, self.bw
         x = m.x_in.data
@@ -302,7 +329,7 @@ class FusedLayer:
         H, Dh, F = m.heads, m.hdim, self.F
         Mrows = B * T
         Tp = (T + 15) // 16 * 16
-        w = ws.get(B, T, Tp, H, Dh, D, F)
+        w = ws.get(B, T, Tp, H, Dh, D, F, unfused_attention=not self.attn_fused)
         call = _lib.call
         # 1) LN1 + quantize (LN1 output feeds the Q/K/V MatMuls)
         call("nqk_ln_quant", x.dev.vp, self.g1.vp, self.be1.vp, w["lnq"].vp, Mrows, D, self.eps1,
@@ -315,21 +342,22 @@ class FusedLayer:
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
                       out=[w["q"].ptr, w["k"].ptr, w["v"].ptr], bias=self.bias_qkv.ptr)
         _gemm(EPI_QKV, w["lnq"], self.bt_qkv, 1, Mrows, 3 * D, D, D, D, None, 0, 0, e)
-        # 3) V -> V^T (the PV GEMM's Bt operand), zero padded to Tp tokens
-        call("nqk_transpose_pad_i8", w["v"].vp, w["vt"].vp, None, B * H, T, Dh, Tp)
-        # 4) scores = dequant(Q K^T) / 8
         pq, pk, pv_ = self.p_head["q"], self.p_head["k"], self.p_head["v"]
-        e = self._epi(zp_flags=_lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST, zpa=_zp(pq), zpb=_zp(pk), kdim=Dh,
-                      s_acc=[_f32(np.float32(pq.scale) * np.float32(pk.scale))], out=[w["s"].ptr], div=m.div)
-        _gemm(EPI_SCORES, w["q"], w["k"], B * H, T, T, Dh, Dh, Dh, None, T * Dh, T * Dh, e)
-        # 5) softmax + quantize (+ row sums for the PV zero-point term)
-        call("nqk_softmax_quant", w["s"].vp, w["p"].vp, None, B * H * T, T, Tp,
-             _f32(self.p_sm.scale), _zp(self.p_sm), bw)
-        # 6) context = dequant(P V) -> Transpose -> Reshape -> quantize
-        e = self._epi(zp_flags=_lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST, zpa=_zp(self.p_sm), zpb=_zp(pv_), kdim=T,
-                      s_acc=[_f32(np.float32(self.p_sm.scale) * np.float32(pv_.scale))],
-                      s_out=[_f32(self.p_ctx.scale)], zp_out=[_zp(self.p_ctx)], out=[w["ctx"].ptr], ld_out=D)
-        _gemm(EPI_PV, w["p"], w["vt"], B * H, T, Dh, Tp, Tp, Tp, None, T * Tp, Dh * Tp, e)
+        if self.attn_fused:
+            # 3-6) one kernel per (image, head): scores, softmax, P V, context quantize
+            a = _lib.Attention()
+            a.heads, a.tokens, a.hdim, a.ld_out, a.bit_width = H, T, Dh, D, bw
+            a.zq, a.zk = _zp(pq), _zp(pk)
+            a.s_qk, a.div = _f32(np.float32(pq.scale) * np.float32(pk.scale)), m.div
+            a.s_p, a.zp_p = _f32(self.p_sm.scale), _zp(self.p_sm)
+            a.s_pv, a.zv = _f32(np.float32(self.p_sm.scale) * np.float32(pv_.scale)), _zp(pv_)
+            a.s_ctx, a.zp_ctx = _f32(self.p_ctx.scale), _zp(self.p_ctx)
+            t0 = KM.TIMER.begin() if KM.TIMER is not None else None
+            call("nqk_attention_fused", w["q"].vp, w["k"].vp, w["v"].vp, w["ctx"].vp, B * H, ctypes.byref(a))
+            if t0 is not None:
+                KM.TIMER.end("attention_fused", t0, (2 * 2 * B * H * T * T * Dh, 3 * B * H * T * Dh + B * T * D))
+        else:
+            self._attention_unfused(w, B, T, Tp, H, Dh, D)
         # 7) output projection + bias + residual
         x1 = DeviceArray((B, T, D), np.float32)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr,
@@ -386,18 +414,22 @@ class Workspace:
         self.key = None
         self.bufs = {}
 
-    def get(self, B, T, Tp, H, Dh, D, F):
+    def get(self, B, T, Tp, H, Dh, D, F, unfused_attention=True):
         key = (B, T, Tp, H, Dh, D, F)
         if key != self.key:
             M = B * T
             self.bufs = {
                 "lnq": DeviceArray((M, D), np.int8), "ln2q": DeviceArray((M, D), np.int8),
                 "q": DeviceArray((B * H * T, Dh), np.int8), "k": DeviceArray((B * H * T, Dh), np.int8),
-                "v": DeviceArray((B * H * T, Dh), np.int8), "vt": DeviceArray((B * H, Dh, Tp), np.int8),
-                "s": DeviceArray((B * H, T, T), np.float32), "p": DeviceArray((B * H, T, Tp), np.int8),
+                "v": DeviceArray((B * H * T, Dh), np.int8),
                 "ctx": DeviceArray((M, D), np.int8), "h": DeviceArray((M, F), np.int8),
             }
             self.key = key
+        if unfused_attention and "s" not in self.bufs:
+            # scores / probabilities of the three-launch attention (not needed by the fused kernel)
+            self.bufs.update({"vt": DeviceArray((B * H, Dh, Tp), np.int8),
+                              "s": DeviceArray((B * H, T, T), np.float32),
+                              "p": DeviceArray((B * H, T, Tp), np.int8)})
         return self.bufs
 
 

@@ -1,0 +1,93 @@
+"""GPU parity of the one-kernel attention (nqk_attention_fused) with the three-launch
+chain it replaces (nqk_qgemm_fused SCORES -> nqk_softmax_quant -> nqk_qgemm_fused PV),
+which tests/test_gpu_plan.py pins to the eager node loop and the reference.  The
+chain is the QModel's MatMul(Q, K^T) -> Div -> Softmax -> MatMul(P, V) -> Transpose
+-> Reshape -> quantize (model.py:486-565).  Integer outputs: bit-exact."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_both(B, H, T, zq, zk, zp, zv, zc, bw=8, seed=0):
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_PV, EPI_SCORES, _gemm
+    rng = np.random.default_rng(seed)
+    lo, hi = -(1 << (bw - 1)), (1 << (bw - 1)) - 1
+    Dh, D = 64, H * 64
+    q = rng.integers(lo, hi + 1, size=(B * H, T, Dh), dtype=np.int8)
+    k = rng.integers(lo, hi + 1, size=(B * H, T, Dh), dtype=np.int8)
+    v = rng.integers(lo, hi + 1, size=(B * H, T, Dh), dtype=np.int8)
+    s_q, s_k, s_v = np.float32(0.031), np.float32(0.027), np.float32(0.043)
+    s_p = np.float32(1.0 / 255)
+    s_ctx = np.float32(0.017)
+    div = 8.0
+    dq, dk, dv = (DeviceArray.from_host(a.reshape(B * H * T, Dh)) for a in (q, k, v))
+    # fused
+    ctx_f = DeviceArray((B, T, D), np.int8)
+    a = _lib.Attention()
+    a.heads, a.tokens, a.hdim, a.ld_out, a.bit_width = H, T, Dh, D, bw
+    a.zq, a.zk, a.s_qk, a.div = zq, zk, float(np.float32(s_q * s_k)), div
+    a.s_p, a.zp_p, a.s_pv, a.zv = float(s_p), zp, float(np.float32(s_p * s_v)), zv
+    a.s_ctx, a.zp_ctx = float(s_ctx), zc
+    _lib.call("nqk_attention_fused", dq.vp, dk.vp, dv.vp, ctx_f.vp, B * H, ctypes.byref(a))
+    # three launches
+    Tp = (T + 15) // 16 * 16
+    vt = DeviceArray((B * H, Dh, Tp), np.int8)
+    s = DeviceArray((B * H, T, T), np.float32)
+    p = DeviceArray((B * H, T, Tp), np.int8)
+    ctx_u = DeviceArray((B, T, D), np.int8)
+    _lib.call("nqk_transpose_pad_i8", dv.vp, vt.vp, None, B * H, T, Dh, Tp)
+    e = _lib.Epilogue()
+    e.bit_width, e.tokens, e.heads, e.hdim = bw, T, H, Dh
+    e.group_cols = 1 << 30
+    e.zp_flags = _lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST
+    e.zpa, e.zpb, e.kdim = zq, zk, Dh
+    e.s_acc[0] = float(np.float32(s_q * s_k))
+    e.out[0] = s.ptr
+    e.div, e.add1, e.mul2 = div, 0.0, 1.0
+    _gemm(EPI_SCORES, dq, dk, B * H, T, T, Dh, Dh, Dh, None, T * Dh, T * Dh, e)
+    _lib.call("nqk_softmax_quant", s.vp, p.vp, None, B * H * T, T, Tp, float(s_p), zp, bw)
+    e2 = _lib.Epilogue()
+    e2.bit_width, e2.tokens, e2.heads, e2.hdim, e2.ld_out = bw, T, H, Dh, D
+    e2.group_cols = 1 << 30
+    e2.zp_flags = _lib.ZP_ROW | _lib.ZP_COL | _lib.ZP_KCONST
+    e2.zpa, e2.zpb, e2.kdim = zp, zv, T
+    e2.s_acc[0] = float(np.float32(s_p * s_v))
+    e2.s_out[0], e2.zp_out[0], e2.out[0] = float(s_ctx), zc, ctx_u.ptr
+    e2.div, e2.add1, e2.mul2 = 1.0, 0.0, 1.0
+    _gemm(EPI_PV, p, vt, B * H, T, Dh, Tp, Tp, Tp, None, T * Tp, Dh * Tp, e2)
+    return ctx_f.to_host(), ctx_u.to_host()
+
+
+@pytest.mark.parametrize("T", [1, 7, 8, 31, 32, 33, 100, 128, 129, 160, 197, 224])
+def test_attention_matches_three_launch_chain(T):
+    f, u = _run_both(2, 3, T, zq=-5, zk=3, zp=-128, zv=2, zc=-7, seed=T)
+    np.testing.assert_array_equal(f, u)
+
+
+@pytest.mark.parametrize("zq,zk,zp,zv,zc,bw", [(0, 0, 0, 0, 0, 8), (-140, 131, -128, -138, 5, 8),
+                                              (4096, -4096, 1024, -1024, 0, 8), (-9, 2, -8, 1, 3, 4)])
+def test_attention_zero_points_and_bit_widths(zq, zk, zp, zv, zc, bw):
+    f, u = _run_both(1, 12, 197, zq, zk, zp, zv, zc, bw=bw, seed=abs(zq) + bw)
+    np.testing.assert_array_equal(f, u)
+
+
+def test_attention_vit_base_batch():
+    """ViT-Base shape at a larger batch (every (image, head) workgroup)."""
+    f, u = _run_both(16, 12, 197, zq=-3, zk=4, zp=-128, zv=-1, zc=2, seed=7)
+    np.testing.assert_array_equal(f, u)
+
+
+def test_attention_rejects_unsupported_shapes():
+    from numpy_quant import _lib
+    a = _lib.Attention()
+    a.heads, a.tokens, a.hdim, a.ld_out, a.bit_width = 1, 225, 64, 64, 8
+    with pytest.raises(_lib.NQKError):
+        _lib.call("nqk_attention_fused", None, None, None, None, 1, ctypes.byref(a))
+    a.tokens, a.hdim = 197, 32
+    with pytest.raises(_lib.NQKError):
+        _lib.call("nqk_attention_fused", None, None, None, None, 1, ctypes.byref(a))
