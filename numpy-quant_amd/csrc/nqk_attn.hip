@@ -11,12 +11,11 @@
 // bit-identical to the unfused chain; only the f32 scores (B*H*T*T*4 bytes) and the
 // int8 probabilities stop travelling through HBM.
 //
-// LDS (T = 197: NT = 7 score tiles of 32 columns, 136 KiB, one workgroup per CU):
-//   Ks   [NT*32][64]     int8, 16-byte chunks XOR-swizzled (conflict-free B reads)
+// LDS (T = 197: NT = 7 score tiles of 32 columns):
+//   Ks   [NT*32][64]     int8, 16-byte chunks XOR-swizzled (conflict-free A reads)
 //   Vt   [64][PST]       int8 V^T, zero padded to NT*32 tokens; PST = NT*32 + 16
-//   csK  [NT*32], csV [64]   int32 row sums of K / column sums of V
-//   per wave: E [32][EST] f32 exp values of its 32-row tile (P aliases it, PST stride)
-//             rsQ [32], rsP [32] row sums of Q / P
+//   colK [NT*32], colV [64]   int32 zero-point column terms
+// 30 KiB per workgroup: two workgroups (8 waves) per CU; everything else is in VGPRs.
 #include "nqk_common.h"
 #include "nqk_numerics.h"
 
@@ -43,68 +42,57 @@ __device__ __forceinline__ int sum16a(v4i c) {
   return __builtin_amdgcn_sdot4(c[3], 0x01010101, s, false);
 }
 
-// RN32(x / c) from rc = RN64(1/c) (see nqk_fused.hip div_rc); the exact division only in
-// a wave-uniform branch for quotients near the subnormal range
-__device__ __forceinline__ float div_rc_w(float x, float c, double rc) {
-  float t = (float)((double)x * rc);
-  const bool slow = __builtin_fabsf(t) < 0x1p-125f && x != 0.0f;
-  if (__builtin_expect(__any(slow), 0)) t = slow ? x / c : t;
-  return t;
-}
+// RN32(x / c) from rc = RN64(1/c): x * rc is within 2^-52 (relative) of x / c while a
+// quotient of two floats is at least 2^-48 away from every float32 rounding midpoint,
+// except for exact midpoints in the subnormal range (|x / c| < 2^-126).  Here every
+// such quotient only feeds a rounding that cannot see it: (a) the scores y = d / div
+// enter exp(y - max), where a |y| < 2^-125 either vanishes next to max or leaves an
+// argument |x| < 2^-24 whose NumPy exp is exactly 1; (b) p = e / sum and t = p / s_p
+// enter rint(zp + t), and |t| < 2^-25 (host check: s >= 2^-100) rounds to zp for any
+// candidate.  So no exact-division fallback is needed (nqk_fused.hip keeps one).
+__device__ __forceinline__ float div_rc_w(float x, double rc) { return (float)((double)x * rc); }
 
 __device__ __forceinline__ int quant_w(float x, float s, double rs, double zp, double lo, double hi) {
-  const float t = div_rc_w(x, s, rs);
+  const float t = div_rc_w(x, rs);
   const double u = zp + (double)t;
   return (int)__builtin_rint(__builtin_fmin(__builtin_fmax(u, lo), hi));
 }
 
-// NumPy pairwise_sum leaf (n <= 128): 8 interleaved accumulators, then the n % 8 tail
-__device__ __forceinline__ float leaf_sum(const float* v, int L) {
-  if (L < 8) {
-    float res = 0.0f;
-    for (int i = 0; i < L; ++i) res = res + v[i];
-    return res;
-  }
-  const float4* v4 = reinterpret_cast<const float4*>(v);
-  float4 a = v4[0], b = v4[1];
-  float r0 = a.x, r1 = a.y, r2 = a.z, r3 = a.w, r4 = b.x, r5 = b.y, r6 = b.z, r7 = b.w;
-  const int end = L - (L % 8);
-  for (int i = 8; i < end; i += 8) {
-    a = v4[i / 4];
-    b = v4[i / 4 + 1];
-    r0 = r0 + a.x; r1 = r1 + a.y; r2 = r2 + a.z; r3 = r3 + a.w;
-    r4 = r4 + b.x; r5 = r5 + b.y; r6 = r6 + b.z; r7 = r7 + b.w;
-  }
-  float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (int i = end; i < L; ++i) res = res + v[i];
-  return res;
+// value of the partner lane (lane ^ 32): one v_permlane32_swap + a select
+__device__ __forceinline__ int xor32i(int x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
 }
+__device__ __forceinline__ float xor32f(float x) { return __int_as_float(xor32i(__float_as_int(x))); }
 
-template <int NT>
-__global__ void __launch_bounds__(256, 1)
+// The scores are computed transposed, S^T = K Q^T (A = K rows from LDS, B = Q rows from
+// HBM), so a lane holds one query row: lane (r32, h) has S[m0 + r32][n] for the 112
+// (NT = 7) key positions n = 32c + 8q + 4h + j' (c < NT, q < 4, j' < 4) of its half
+// and the partner lane (lane ^ 32) has the other half.  Row max, NumPy's pairwise sum
+// (accumulator j = n % 8 lives in half j / 4; chains in increasing n), division and
+// quantize are all in-lane; one cross-half exchange combines them.  The context is
+// computed transposed as well (O^T = V^T P^T), so each lane stores 4 consecutive
+// head dimensions of its query row at once.
+template <int NT, int TC>  // TC: compile-time token count (0: runtime a.T)
+__global__ void __launch_bounds__(256, 2)
 k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int8_t* __restrict__ Vg,
             int8_t* __restrict__ ctx, AttnArgs a) {
   constexpr int TP = NT * 32;  // padded tokens (score columns / PV contraction)
+  constexpr int G = TP / 8;    // 8-column groups of a score row
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
-  const int T = a.T, PST = a.PST, EST = a.EST;
+  const int T = TC ? TC : a.T, PST = TC ? NT * 32 + 16 : a.PST;
   int8_t* Ks = lds;
   int8_t* Vt = Ks + TP * 64;
-  int* csK = reinterpret_cast<int*>(Vt + 64 * PST);
-  int* csV = csK + TP;
+  int* colK = reinterpret_cast<int*>(Vt + 64 * PST);  // rowsum(K[n]) * zq - zq*zk*64
+  int* colV = colK + TP;                              // colsum(V[:, d]) * zp - zp*zv*T
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int8_t* wreg = reinterpret_cast<int8_t*>(csV + 64) + wave * (32 * EST * 4 + 256);
-  float* E = reinterpret_cast<float*>(wreg);
-  int8_t* P = wreg;  // aliases E row by row (P row r ends before E row r + 1 starts)
-  int* rsQ = reinterpret_cast<int*>(wreg + 32 * EST * 4);
-  int* rsP = rsQ + 32;
-
   const int bh = blockIdx.x;
   const int img = bh / a.H, head = bh - img * a.H;
   const int8_t* q = Qg + (int64_t)bh * T * 64;
   const int8_t* k = Kg + (int64_t)bh * T * 64;
   const int8_t* v = Vg + (int64_t)bh * T * 64;
 
-  // ---- K (swizzled) and V^T (zero padded) into LDS
+  // ---- K (swizzled) and V^T (zero padded) into LDS, zero-point column terms
   for (int idx = tid; idx < TP * 4; idx += 256) {
     const int row = idx >> 2, ch = idx & 3;
     const v4i z = {0, 0, 0, 0};
@@ -119,7 +107,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   __syncthreads();
   for (int row = tid; row < TP; row += 256) {
     const v4i* kr = reinterpret_cast<const v4i*>(Ks + row * 64);
-    csK[row] = sum16a(kr[0]) + sum16a(kr[1]) + sum16a(kr[2]) + sum16a(kr[3]);
+    colK[row] = (sum16a(kr[0]) + sum16a(kr[1]) + sum16a(kr[2]) + sum16a(kr[3])) * a.zq - a.kq;
   }
   {
     const int d = tid >> 2, part = tid & 3;
@@ -127,23 +115,32 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     for (int c = part; c < NT * 2; c += 4) s += sum16a(*reinterpret_cast<const v4i*>(Vt + d * PST + c * 16));
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
-    if (part == 0) csV[d] = s;
+    if (part == 0) colV[d] = s * a.zp - a.kp;
   }
   __syncthreads();
 
-  const int r32 = lane & 31, half = lane >> 5;
+  // pairwise-sum plan of a row (uniform): leaf l = [s0_l, s0_l + L_l), main part of
+  // ng_l whole 8-groups from group g0_l, then a tail of tl_l < 8 columns
+  const int n2 = TC ? (TC > 128 ? (TC / 2) - (TC / 2) % 8 : 0) : a.n2;
+  const int L0 = n2 ? n2 : T, L1 = n2 ? T - n2 : 0;
+  const int g0_0 = 0, g0_1 = n2 >> 3;
+  const int ng0 = L0 >= 8 ? L0 >> 3 : 0, ng1 = L1 >= 8 ? L1 >> 3 : 0;
+  const int tl0 = L0 - 8 * ng0, tl1 = L1 - 8 * ng1;
+  const int gt0 = g0_0 + ng0, gt1 = g0_1 + ng1;  // tail groups
+
+  const int r32 = lane & 31, h = lane >> 5;
   for (int rt = wave; rt < NT; rt += 4) {
-    const int m0 = rt * 32;
-    // ---- S = Q K^T (raw int32) for rows m0..m0+31, all TP columns
-    v4i qa[2];
+    const int m0 = rt * 32, m = m0 + r32;
+    v4i qb[2];
     {
-      const int qrow = min(m0 + r32, T - 1);
-      qa[0] = *reinterpret_cast<const v4i*>(q + qrow * 64 + half * 16);
-      qa[1] = *reinterpret_cast<const v4i*>(q + qrow * 64 + (2 + half) * 16);
+      const int qrow = min(m, T - 1);
+      qb[0] = *reinterpret_cast<const v4i*>(q + qrow * 64 + h * 16);
+      qb[1] = *reinterpret_cast<const v4i*>(q + qrow * 64 + (2 + h) * 16);
     }
-    int rq = sum16a(qa[0]) + sum16a(qa[1]);
-    rq += __shfl_xor(rq, 32, 64);
-    if (half == 0) rsQ[r32] = rq;
+    int rq = sum16a(qb[0]) + sum16a(qb[1]);
+    rq += xor32i(rq);
+    const int rowterm = rq * a.zk;
+    // ---- S^T = K Q^T
     v16i acc[NT];
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
@@ -151,111 +148,146 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
       for (int r = 0; r < 16; ++r) acc[c][r] = 0;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const v4i kb = *reinterpret_cast<const v4i*>(Ks + swz64a(c * 32 + r32, 2 * s + half));
-        acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(qa[s], kb, acc[c], 0, 0, 0);
+        const v4i ka = *reinterpret_cast<const v4i*>(Ks + swz64a(c * 32 + r32, 2 * s + h));
+        acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ka, qb[s], acc[c], 0, 0, 0);
       }
     }
-    wave_lds_sync();
-    // ---- dequant + Div (EPI_SCORES), row max, NumPy exp -> E
-    float y[NT][16];
+    // ---- dequant + Div (EPI_SCORES), row max
+    float e[NT][16];
+    float mx = -__builtin_inff();
 #pragma unroll
-    for (int c = 0; c < NT; ++c) {
-      const int col = c * 32 + r32;
-      const int colterm = csK[col] * a.zq - a.kq;
+    for (int c = 0; c < NT; ++c)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const v4i ck = *reinterpret_cast<const v4i*>(colK + c * 32 + 8 * qq + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * qq + j, n = c * 32 + 8 * qq + 4 * h + j;
+          const int vv = acc[c][r] - rowterm - ck[j];
+          const float d = (float)((double)vv * (double)a.s_qk);
+          // -inf for padded columns: an add of a selected constant, so no branch
+          const float y = div_rc_w(d, a.rdiv) + (n < T ? 0.0f : -__builtin_inff());
+          e[c][r] = y;
+          mx = y > mx ? y : mx;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    {
+      const float o = xor32f(mx);
+      mx = o > mx ? o : mx;
+    }
+    const float nm = -mx;
+#pragma unroll
+    for (int c = 0; c < NT; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
-        const int vv = acc[c][r] - rsQ[row] * a.zk - colterm;
-        const float d = (float)((double)vv * (double)a.s_qk);
-        const float yy = div_rc_w(d, a.div, a.rdiv);
-        y[c][r] = col < T ? yy : -__builtin_inff();
+        e[c][r] = np_expf(e[c][r] + nm);  // -inf pads -> 0
+        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+    // ---- NumPy pairwise sum: accumulators r[4h + j] of each leaf, in increasing n
+    float ra[2][4], tv[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ra[0][j] = ra[1][j] = tv[0][j] = tv[1][j] = 0.0f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int c = g >> 2, qq = g & 3;
+      const bool f0 = g == g0_0, in0 = g < g0_0 + ng0;
+      const bool f1 = g == g0_1, in1 = g >= g0_1 && g < g0_1 + ng1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = e[c][4 * qq + j];
+        ra[0][j] = in0 ? (f0 ? x : ra[0][j] + x) : ra[0][j];
+        ra[1][j] = in1 ? (f1 ? x : ra[1][j] + x) : ra[1][j];
+        tv[0][j] = g == gt0 ? x : tv[0][j];
+        tv[1][j] = g == gt1 ? x : tv[1][j];
       }
     }
+    float leaf[2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float mx = y[0][r];
-#pragma unroll
-      for (int c = 1; c < NT; ++c) mx = y[c][r] > mx ? y[c][r] : mx;
-#pragma unroll
-      for (int off = 1; off < 32; off <<= 1) {
-        const float o = __shfl_xor(mx, off, 64);
-        mx = o > mx ? o : mx;
+    for (int l = 0; l < 2; ++l) {
+      const int ng = l ? ng1 : ng0, tl = l ? tl1 : tl0;
+      float res = 0.0f;
+      if (ng > 0) {
+        const float mine = (ra[l][0] + ra[l][1]) + (ra[l][2] + ra[l][3]);
+        const float other = xor32f(mine);
+        res = h ? other + mine : mine + other;
       }
-      const float nm = -mx;
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+      // tail columns t < tl: t = 0..3 in half 0, 4..7 in half 1, added in order
+      float x = res;
 #pragma unroll
-      for (int c = 0; c < NT; ++c) {
-        const int col = c * 32 + r32;
-        if (col < T) E[row * EST + col] = np_expf(y[c][r] + nm);
-      }
+      for (int t = 0; t < 4; ++t)
+        if (t < tl) x = x + tv[l][t];
+      const float x0 = xor32f(x);  // half 1 receives half 0's running sum
+      float y = x0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (4 + t < tl) y = y + tv[l][t];
+      const float y1 = xor32f(y);  // half 0 receives half 1's result
+      leaf[l] = h ? y : y1;
     }
-    wave_lds_sync();
-    // ---- NumPy pairwise row sums: lane = (row, leaf)
-    float tot;
-    {
-      const int s0 = half ? a.n2 : 0;
-      const int L = a.n2 ? (half ? T - a.n2 : a.n2) : (half ? 0 : T);
-      const float res = leaf_sum(E + r32 * EST + s0, L);
-      const float other = __shfl_xor(res, 32, 64);
-      tot = a.n2 ? (half ? other + res : res + other) : (half ? other : res);
-    }
-    // ---- P = quantize(E / sum), one row per step (lane: 4 columns), int8 into P
-    const int c0 = lane * 4;
-    for (int r = 0; r < 32; ++r) {
-      if (m0 + r >= T) break;
-      const float ssum = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tot), r));
-      const double rsum = 1.0 / (double)ssum;
-      if (c0 < TP) {
-        float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (c0 < T) e4 = *reinterpret_cast<const float4*>(E + r * EST + c0);
-        const float ev[4] = {e4.x, e4.y, e4.z, e4.w};
+    const float tot = n2 ? leaf[0] + leaf[1] : leaf[0];
+    const double rtot = 1.0 / (double)tot;
+    // ---- P = quantize(e / tot): 4 packed bytes per (tile, group), row sums
+    int dw[NT][4];
+    int rp = 0;
+#pragma unroll
+    for (int c = 0; c < NT; ++c)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
         uint32_t packed = 0;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          int qv = 0;
-          if (c0 + kk < T) qv = quant_w(div_rc_w(ev[kk], ssum, rsum), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi);
-          packed |= ((uint32_t)(qv & 0xff)) << (8 * kk);
+        for (int j = 0; j < 4; ++j) {
+          const int n = c * 32 + 8 * qq + 4 * h + j;
+          const int qv = quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) &
+                         -(int)(n < T);  // padded columns: 0
+          rp += qv;
+          packed |= ((uint32_t)(qv & 0xff)) << (8 * j);
         }
-        *reinterpret_cast<uint32_t*>(P + r * PST + c0) = packed;
+        dw[c][qq] = (int)packed;
+        __builtin_amdgcn_sched_barrier(0);
       }
-    }
-    wave_lds_sync();
-    // ---- ctx = P V (raw int32), P row sums
+    rp += xor32i(rp);
+    // ---- O^T = V^T P^T: B operand = P row m, 16 consecutive tokens per half
     v16i acc2[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc2[j][r] = 0;
-    int rp = 0;
 #pragma unroll
-    for (int s = 0; s < NT; ++s) {
-      const v4i pa = *reinterpret_cast<const v4i*>(P + r32 * PST + (2 * s + half) * 16);
-      rp += sum16a(pa);
+    for (int c = 0; c < NT; ++c) {
+      // half 0 needs tokens 0..15 of the tile = [own g0, partner g0, own g1, partner g1];
+      // half 1 needs 16..31 = [partner g2, own g2, partner g3, own g3]
+      const int xa = xor32i(h ? dw[c][0] : dw[c][2]);
+      const int xb = xor32i(h ? dw[c][1] : dw[c][3]);
+      v4i pb;
+      if (h) { pb[0] = xa; pb[1] = dw[c][2]; pb[2] = xb; pb[3] = dw[c][3]; }
+      else   { pb[0] = dw[c][0]; pb[1] = xa; pb[2] = dw[c][1]; pb[3] = xb; }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const v4i vb = *reinterpret_cast<const v4i*>(Vt + (j * 32 + r32) * PST + (2 * s + half) * 16);
-        acc2[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(pa, vb, acc2[j], 0, 0, 0);
+        const v4i va = *reinterpret_cast<const v4i*>(Vt + (j * 32 + r32) * PST + (2 * c + h) * 16);
+        acc2[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(va, pb, acc2[j], 0, 0, 0);
       }
     }
-    rp += __shfl_xor(rp, 32, 64);
-    wave_lds_sync();
-    if (half == 0) rsP[r32] = rp;
-    wave_lds_sync();
-    // ---- dequant + quantize (EPI_PV) -> ctx[img][token][head * 64 + d]
+    // ---- dequant + quantize (EPI_PV) -> ctx[img][m][head * 64 + d], 4 dims per store
+    const int rowp = rp * a.zv;
+    int8_t* orow = ctx + ((int64_t)img * T + m) * a.ld_out + head * 64;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int d = j * 32 + r32;
-      const int colterm = csV[d] * a.zp - a.kp;
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
-        const int vv = acc2[j][r] - rsP[row] * a.zv - colterm;
-        const float o = (float)((double)vv * (double)a.s_pv);
-        const int qv = quant_w(o, a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
-        if (m0 + row < T) ctx[((int64_t)img * T + m0 + row) * a.ld_out + head * 64 + d] = (int8_t)qv;
+      for (int qq = 0; qq < 4; ++qq) {
+        const int d0 = j * 32 + 8 * qq + 4 * h;
+        const v4i cv = *reinterpret_cast<const v4i*>(colV + d0);
+        uint32_t packed = 0;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int vv = acc2[j][4 * qq + jj] - rowp - cv[jj];
+          const float o = (float)((double)vv * (double)a.s_pv);
+          const int qv = quant_w(o, a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
+          packed |= ((uint32_t)(qv & 0xff)) << (8 * jj);
+        }
+        if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
+        __builtin_amdgcn_sched_barrier(0);
       }
-    }
-    wave_lds_sync();
   }
 }
 
@@ -277,6 +309,10 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   if (!small(p->zq, 4096) || !small(p->zk, 4096) || !small(p->zp_p, 1024) || !small(p->zv, 1024))
     return fail("nqk_attention_fused: zero points beyond the int32-exact range");
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v)) & 15) return fail("nqk_attention_fused: unaligned Q/K/V");
+  if ((((uintptr_t)ctx) & 3) || (p->ld_out & 3)) return fail("nqk_attention_fused: ctx / ld_out not 4-byte aligned");
+  auto normal = [](float x) { return __builtin_fabsf(x) >= 0x1p-100f && __builtin_fabsf(x) <= 0x1p100f; };
+  if (!normal(p->s_p) || !normal(p->s_ctx) || !normal(p->div))
+    return fail("nqk_attention_fused: scales / divisor outside [2^-100, 2^100]");
   if (batch_heads > 0x7fffffff) return fail("nqk_attention_fused: too many (image, head) pairs");
   const int NT = (T + 31) / 32;
   AttnArgs a{};
@@ -310,11 +346,13 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   a.zp_ctx = (double)p->zp_ctx;
   a.lo = -__builtin_ldexp(1.0, p->bit_width - 1);
   a.hi = __builtin_ldexp(1.0, p->bit_width - 1) - 1.0;
-  const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + (size_t)(NT * 32 + 64) * 4 +
-                     4 * ((size_t)32 * a.EST * 4 + 256);
+  const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + (size_t)(NT * 32 + 64) * 4;
   const dim3 grid((unsigned)batch_heads);
-  switch (NT) {
-#define A(n) case n: hipLaunchKernelGGL(k_attention<n>, grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;
+  switch (T == 197 ? 0 : NT) {
+#define A(n) case n: hipLaunchKernelGGL((k_attention<n, 0>), grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;
+    case 0:  // ViT at 224 px (196 patches + CLS): the pairwise plan and pads fold at compile time
+      hipLaunchKernelGGL((k_attention<7, 197>), grid, dim3(256), shm, stream(), q, k, v, ctx, a);
+      break;
     A(1) A(2) A(3) A(4) A(5) A(6) A(7)
 #undef A
     default: return fail("nqk_attention_fused: bad tile count");

@@ -10,7 +10,6 @@ namespace {
 // ------------------------------------------------------------------ numpy float32 exp
 __device__ __forceinline__ float np_expf(float x) {
   const float xmax = 88.72283935546875f, xmin = -103.97208404541015625f;
-  if (x != x) return x;
   const bool over = x >= xmax, under = x <= xmin;
   float xx = (over || under) ? 0.0f : x;
   float q = xx * 1.442695040888963407359924681001892137f;
@@ -28,9 +27,9 @@ __device__ __forceinline__ float np_expf(float x) {
   den = __builtin_fmaf(den, r, 1.0f);
   float poly = num / den;
   poly = __builtin_ldexpf(poly, (int)q);
-  if (over) poly = __builtin_inff();
-  if (under) poly = 0.0f;
-  return poly;
+  poly = over ? __builtin_inff() : poly;
+  poly = under ? 0.0f : poly;
+  return x != x ? x : poly;  // NaN passes through (selects, no branch)
 }
 
 // numpy_helper.py:95-112 (A&S 7.1.26), float32 throughout
