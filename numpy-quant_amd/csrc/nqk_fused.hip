@@ -587,6 +587,58 @@ k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float
   }
 }
 
+// LayerNorm + quantize with the whole NumPy pairwise tree in registers, for rows whose
+// plan is a complete binary tree of NL equal leaves of LF (multiple of 8) columns
+// (768 = 8 x 96 for ViT-Base): lane (leaf, j) owns columns leaf*LF + j + 8i, i.e.
+// exactly NumPy's accumulator r[j] of that leaf, summed in increasing i; the
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) combine and the leaf tree are xor-butterflies
+// (float addition is commutative, only the grouping matters).  One row per NL*8 lanes.
+template <int NL, int LF>
+__global__ void __launch_bounds__(256)
+k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
+               int8_t* __restrict__ out, int64_t rows, float eps, float s, double rs, double zp, double lo,
+               double hi) {
+  constexpr int LPR = NL * 8, NI = LF / 8, COLS = NL * LF;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  const int u = lane % LPR, leaf = u >> 3, j = u & 7;
+  const bool ok = row < rows;
+  const float* xr = x + (ok ? row : 0) * COLS + leaf * LF + j;
+  float xv[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) xv[i] = xr[8 * i];
+  float acc = xv[0];
+#pragma unroll
+  for (int i = 1; i < NI; ++i) acc = acc + xv[i];
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) acc = acc + __shfl_xor(acc, m, 64);
+  const float fcols = (float)COLS;
+  const float mean = acc / fcols;
+  const float nmean = -mean;
+  float dv[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) dv[i] = xv[i] + nmean;
+  float v2 = dv[0] * dv[0];
+#pragma unroll
+  for (int i = 1; i < NI; ++i) v2 = v2 + dv[i] * dv[i];
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) v2 = v2 + __shfl_xor(v2, m, 64);
+  const float var = v2 / fcols;
+  const float inv = 1.0f / __builtin_sqrtf(var + eps);
+  if (!ok) return;
+  int8_t* orow = out + row * COLS + leaf * LF + j;
+  const float* gg = g + leaf * LF + j;
+  const float* bb = b + leaf * LF + j;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const float y = ((dv[i] * inv) * gg[8 * i]) + bb[8 * i];
+    const float t = (float)((double)y * rs);
+    const double uu = zp + (double)t;
+    const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
+    orow[8 * i] = (int8_t)q;
+  }
+}
+
 // ------------------------------------------------------------------ Softmax + quantize
 // one row per wave; output row stride ldo (>= cols, pad zero-filled); optional row sums
 __global__ void __launch_bounds__(256)
@@ -766,6 +818,26 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
   PwPlan p;
   if (row_plan(cols, p)) return -1;
   const double lo = -__builtin_ldexp(1.0, bit_width - 1), hi = __builtin_ldexp(1.0, bit_width - 1) - 1.0;
+  // register-tree kernel: balanced plan of equal leaves of 96 columns (768 = ViT-Base,
+  // 192 = ViT-Tiny, 384 = ViT-Small); the quotient t = y / s only feeds rint(zp + t), so
+  // the RN64(1/s) product needs no subnormal fallback (see nqk_attn.hip div_rc_w)
+  bool eq = p.balanced && p.nleaf >= 1;
+  for (int l = 0; eq && l < p.nleaf; ++l) eq = p.len[l] == 96;
+  const bool snormal = __builtin_fabsf(scale) >= 0x1p-100f && __builtin_fabsf(scale) <= 0x1p100f;
+  if (eq && snormal && (p.nleaf == 8 || p.nleaf == 4 || p.nleaf == 2)) {
+    const double rs = 1.0 / (double)scale;
+    const int64_t lanes = rows * p.nleaf * 8;
+    const unsigned grid = (unsigned)((lanes + 255) / 256);
+    switch (p.nleaf) {
+      case 8: hipLaunchKernelGGL((k_ln_quant_reg<8, 96>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
+                                 eps, scale, rs, (double)zp, lo, hi); break;
+      case 4: hipLaunchKernelGGL((k_ln_quant_reg<4, 96>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
+                                 eps, scale, rs, (double)zp, lo, hi); break;
+      default: hipLaunchKernelGGL((k_ln_quant_reg<2, 96>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out,
+                                  rows, eps, scale, rs, (double)zp, lo, hi); break;
+    }
+    return launch_status("nqk_ln_quant(reg)");
+  }
   const int64_t slice = (int64_t)(row_smem(cols) / sizeof(float) + 3) / 4 * 4;
   const unsigned grid = (unsigned)(((rows + 3) / 4) < 65536 * 4 ? (rows + 3) / 4 : 65536 * 4);
   hipLaunchKernelGGL(k_ln_quant, dim3(grid), dim3(256), 4 * slice * sizeof(float), stream(), x, gamma, beta, out,

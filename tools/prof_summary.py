@@ -10,7 +10,7 @@ top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
 agg = collections.defaultdict(list)
 for r in rows:
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    name = r["Kernel_Name"].split("(")[0].replace("nqk::(anonymous namespace)::", "").replace("void ", "")
+    name = r["Kernel_Name"].replace("nqk::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
     agg[(name[:48], r["Grid_Size_X"], r["Grid_Size_Z"])].append(d)
 tot = sum(sum(v) for v in agg.values())
 for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:top]:
