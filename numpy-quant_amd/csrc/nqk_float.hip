@@ -39,13 +39,33 @@ __global__ void k_add_scalar(const float* __restrict__ x, float s, float* __rest
 }
 
 struct Nd {
-  int ndim;
+  int ndim, small;  // small: every index and extent < 2^31 -> 32-bit magic-number divmod
   int64_t shape[6];
   int64_t s0[6], s1[6], s2[6];
+  uint32_t mag[6], ext[6];
+  int sh1[6], sh2[6];
 };
+
+// n / d for 32-bit unsigned n with a precomputed magic (Granlund-Montgomery round-up)
+__device__ __forceinline__ uint32_t magic_div(uint32_t n, uint32_t mag, int sh1, int sh2) {
+  const uint32_t t = __umulhi(mag, n);
+  return (t + ((n - t) >> sh1)) >> sh2;
+}
 
 __device__ __forceinline__ void nd_offsets(const Nd& d, int64_t i, int64_t& o0, int64_t& o1, int64_t& o2) {
   o0 = o1 = o2 = 0;
+  if (d.small) {
+    uint32_t u = (uint32_t)i;
+    for (int k = d.ndim - 1; k >= 0; --k) {
+      const uint32_t q = magic_div(u, d.mag[k], d.sh1[k], d.sh2[k]);
+      const int64_t c = (int64_t)(u - q * d.ext[k]);
+      u = q;
+      o0 += c * d.s0[k];
+      o1 += c * d.s1[k];
+      o2 += c * d.s2[k];
+    }
+    return;
+  }
   for (int k = d.ndim - 1; k >= 0; --k) {
     int64_t c = i % d.shape[k];
     i /= d.shape[k];
@@ -229,14 +249,39 @@ __global__ void __launch_bounds__(256) k_minmax_final(const float* __restrict__ 
   }
 }
 
+// drop extent-1 dimensions and merge neighbours that are contiguous for every operand
+// (the output / destination index is always row-major), then precompute magic divisors
 Nd make_nd(int ndim, const int64_t* shape, const int64_t* s0, const int64_t* s1, const int64_t* s2) {
   Nd d{};
-  d.ndim = ndim;
+  int n = 0;
   for (int k = 0; k < ndim; ++k) {
-    d.shape[k] = shape[k];
-    d.s0[k] = s0 ? s0[k] : 0;
-    d.s1[k] = s1 ? s1[k] : 0;
-    d.s2[k] = s2 ? s2[k] : 0;
+    if (shape[k] == 1) continue;
+    const int64_t a0 = s0 ? s0[k] : 0, a1 = s1 ? s1[k] : 0, a2 = s2 ? s2[k] : 0;
+    if (n > 0 && d.s0[n - 1] == a0 * shape[k] && d.s1[n - 1] == a1 * shape[k] && d.s2[n - 1] == a2 * shape[k]) {
+      d.shape[n - 1] *= shape[k];
+      d.s0[n - 1] = a0;
+      d.s1[n - 1] = a1;
+      d.s2[n - 1] = a2;
+      continue;
+    }
+    d.shape[n] = shape[k];
+    d.s0[n] = a0;
+    d.s1[n] = a1;
+    d.s2[n] = a2;
+    ++n;
+  }
+  d.ndim = n;
+  int64_t total = 1;
+  for (int k = 0; k < n; ++k) total *= d.shape[k];
+  d.small = total < (int64_t(1) << 31);
+  for (int k = 0; k < n && d.small; ++k) {
+    const uint32_t dv = (uint32_t)d.shape[k];
+    int l = 0;
+    while ((uint64_t(1) << l) < dv) ++l;
+    d.mag[k] = (uint32_t)(((uint64_t(1) << 32) * ((uint64_t(1) << l) - dv)) / dv + 1);
+    d.sh1[k] = l < 1 ? l : 1;
+    d.sh2[k] = l > 1 ? l - 1 : 0;
+    d.ext[k] = dv;
   }
   return d;
 }
