@@ -82,19 +82,55 @@ def build_qmodel(batch: int, bit_width: int, group=None, calib_batch: int = 8):
     return model, qmodel
 
 
-def gemm_roofline(qmodel, x_dev):
-    """Time every int8 MFMA GEMM launch of one forward with stream events."""
+PROJ_TAGS = ("qgemm_qkv", "qgemm_resid", "qgemm_gelu")  # MatMuls with constant weights (k_qgemm_big)
+
+
+def kernel_breakdown(qmodel, x_dev):
+    """One extra forward with every fused launch bracketed by events on the library
+    stream (the stream the kernels run on): per tag launches, average duration and
+    achieved rate (int8 ops for MFMA kernels, algorithmic bytes for HBM-bound ones)."""
     from numpy_quant import kernels as K
     K.TIMER = K.KernelTimer()
     qmodel.set_inputs([x_dev])
     qmodel.run()
-    recs = [r for r in K.TIMER.collect()]
+    recs = K.TIMER.collect()
     K.TIMER = None
-    ms = sum(r[1] for r in recs)
-    ops = sum(r[2][0] for r in recs)
-    byts = sum(r[2][1] for r in recs)
-    return {"launches": len(recs), "ms": ms, "ops": ops, "bytes": byts,
-            "avg_launch_us": 1e3 * ms / max(1, len(recs))}
+    by = {}
+    for tag, ms, (ops, byts) in recs:
+        d = by.setdefault(tag, {"launches": 0, "ms": 0.0, "ops": 0, "bytes": 0})
+        d["launches"] += 1
+        d["ms"] += ms
+        d["ops"] += ops
+        d["bytes"] += byts
+    out = {}
+    for tag, d in sorted(by.items(), key=lambda kv: -kv[1]["ms"]):
+        e = {"launches": d["launches"], "avg_us": round(1e3 * d["ms"] / d["launches"], 2),
+             "ms_per_forward": round(d["ms"], 3)}
+        if d["ops"]:
+            tops = d["ops"] / (d["ms"] * 1e-3) / 1e12
+            e.update(achieved=round(tops, 1), unit="TOPS int8", frac=round(tops / INT8_PEAK_TOPS, 4))
+        else:
+            gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+            e.update(achieved=round(gbs, 1), unit="GB/s", frac=round(gbs / HBM_PEAK_GBS, 4))
+        out[tag] = e
+    proj = [by[t] for t in PROJ_TAGS if t in by]
+    pm = sum(d["ms"] for d in proj)
+    po = sum(d["ops"] for d in proj)
+    pl = sum(d["launches"] for d in proj)
+    return out, {"ms": pm, "ops": po, "launches": pl}
+
+
+def traffic_from_profiles(kernel_prefix: str):
+    """HBM bytes per launch of the projection GEMMs from the committed PMC summary
+    (profiles/*_pmc_traffic.json, collected with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    in separate passes, FETCH_SIZE doubled for gfx950 per MI355X_MICROARCH.md), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        data = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    ent = data.get("kernels", {}).get(kernel_prefix)
+    return None if ent is None else ent.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(bit_width: int) -> dict:
@@ -173,10 +209,10 @@ def main():
     samples = args.batch * world * args.steps
     value = samples / dt
 
-    roof = gemm_roofline(qmodel, x_dev)
+    kern, proj = kernel_breakdown(qmodel, x_dev)
     res = None
     if rank == 0:
-        achieved = roof["ops"] / (roof["ms"] * 1e-3) / 1e12
+        achieved = proj["ops"] / (proj["ms"] * 1e-3) / 1e12
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -197,10 +233,13 @@ def main():
                        "parallelism": f"replicas x{world}", "executor": "eager" if args.eager else "fused plan"},
             "matmul_tops": round(achieved, 2),
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(INT8_PEAK_TOPS, 1),
-                         "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4), "traffic": None,
-                         "kernel": "int8 MFMA GEMMs of one forward (k_qgemm_epi fused epilogues + k_qgemm_i8)",
-                         "launches": roof["launches"], "avg_launch_us": round(roof["avg_launch_us"], 2),
-                         "gemm_ms_per_forward": round(roof["ms"], 3)},
+                         "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4),
+                         "traffic": traffic_from_profiles("k_qgemm_big"),
+                         "kernel": "k_qgemm_big: the 48 int8 MFMA projection GEMMs of one forward (QKV, attention "
+                                   "output, FFN up + GELU, FFN down; fused epilogues), 2*M*N*K int8 ops per launch",
+                         "launches": proj["launches"], "avg_launch_us": round(1e3 * proj["ms"] / max(1, proj["launches"]), 2),
+                         "gemm_ms_per_forward": round(proj["ms"], 3)},
+            "kernels": kern,
         }
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args.bit_width)

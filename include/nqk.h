@@ -224,6 +224,11 @@ typedef struct nqk_attention {
 int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_t* v, int8_t* ctx, int64_t batch_heads,
                         const nqk_attention* params);
 
+/* Diagnostic: on the device, compares the fast-division variants of NumPy's exp and the
+ * reference's erf (used by the fused kernels) with the IEEE-division ones on all 2^32
+ * float inputs; adds the mismatch counts to counts_dev[0] (exp) / [1] (erf). */
+int nqk_selftest_fastmath(unsigned long long* counts_dev, uint32_t* examples_dev);
+
 /* ------------------------------------------------ multi-GPU replicas (RCCL) */
 int nqk_comm_unique_id(void* id128);                         /* rank 0 */
 int nqk_comm_init(const void* id128, int nranks, int rank);

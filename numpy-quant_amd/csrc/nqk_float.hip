@@ -249,6 +249,22 @@ __global__ void __launch_bounds__(256) k_minmax_final(const float* __restrict__ 
   }
 }
 
+// exhaustive check: fast vs IEEE-division variants of np_expf / ref_erf on all 2^32
+// bit patterns; counts[0] / counts[1] = mismatching exp / erf inputs, ex[0..1] = an example
+__global__ void k_fastmath_check(unsigned long long* counts, uint32_t* ex) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned long long ce = 0, cr = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t(1) << 32); i += stride) {
+    const float x = __uint_as_float((uint32_t)i);
+    const float a = np_expf_t<true>(x), b = np_expf_t<false>(x);
+    if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) { ++ce; ex[0] = (uint32_t)i; }
+    const float c = ref_erf_t<true>(x), d = ref_erf_t<false>(x);
+    if (__float_as_uint(c) != __float_as_uint(d) && !(c != c && d != d)) { ++cr; ex[1] = (uint32_t)i; }
+  }
+  if (ce) atomicAdd(counts, ce);
+  if (cr) atomicAdd(counts + 1, cr);
+}
+
 // drop extent-1 dimensions and merge neighbours that are contiguous for every operand
 // (the output / destination index is always row-major), then precompute magic divisors
 Nd make_nd(int ndim, const int64_t* shape, const int64_t* s0, const int64_t* s1, const int64_t* s2) {
@@ -312,6 +328,11 @@ extern "C" int nqk_binary_f32(int op, const float* a, const float* b, float* out
     default: return fail("nqk_binary_f32: bad op");
   }
   return launch_status("nqk_binary_f32");
+}
+
+extern "C" int nqk_selftest_fastmath(unsigned long long* counts_dev, uint32_t* examples_dev) {
+  hipLaunchKernelGGL(k_fastmath_check, dim3(256 * 64), dim3(256), 0, stream(), counts_dev, examples_dev);
+  return launch_status("nqk_selftest_fastmath");
 }
 
 extern "C" int nqk_unary_f32(int op, const float* x, float* out, int64_t n) {

@@ -182,13 +182,14 @@ __device__ __forceinline__ EpiCol4 epi_col4(const Epi& e, int gn0, bool ok) {
   return c;
 }
 
-// RN32(x / c) as div_rc, with the (exact) f32 division taken only in a wave-uniform
-// branch when some lane's quotient is near the subnormal range (never on these paths)
+// RN32(x / c) from rc = RN64(1/c) without div_rc's subnormal fallback.  Used by the
+// big-tile epilogues only for quotients whose exact rounding below 2^-125 cannot reach
+// the output (nqk_attn.hip div_rc_w): t = y / s_out feeds rint(zp + t) (host check:
+// s_out in [2^-100, 2^100]), and GELU's h / sqrt(2) feeds erf(), whose value for any
+// |x| < 2^-125 only perturbs h * (erf + 1) * 0.5 at |h| < 2^-124, which quantizes to zp.
 __device__ __forceinline__ float div_rc_u(float x, float c, double rc) {
-  float t = (float)((double)x * rc);
-  const bool slow = __builtin_fabsf(t) < 0x1p-125f && x != 0.0f;
-  if (__builtin_expect(__any(slow), 0)) t = slow ? x / c : t;
-  return t;
+  (void)c;
+  return (float)((double)x * rc);
 }
 
 // quantize (numpy_quantization.py:24-34) with max/min clipping: a NaN clips to lo, as
@@ -397,21 +398,31 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
 // vmcnt waits and raw s_barriers.  The LDS image is lane-linear per 1 KiB piece; the
 // conflict-free chunk swizzle is applied to the SOURCE address.  Needs K % 64 == 0
 // and precomputed weight column sums (zero-point COL term only).
-constexpr int GBM = 128, GBN = 256, GBK = 64, GST = 3;
-constexpr int GSTAGE = (GBM + GBN) * GBK;  // 24 KiB
-constexpr int GAP = GBM * GBK / 1024 / 4;  // A pieces per wave per stage (2)
-constexpr int GBP = GBN * GBK / 1024 / 4;  // B pieces per wave per stage (4)
-constexpr int GPW = GAP + GBP;             // glds per wave per stage (6)
+constexpr int GBN = 256, GBK = 64, GST = 3;
+
+// WR wave rows: 1 -> 128x256 tile, 4 waves (1x4), two blocks per CU;
+//               2 -> 256x256 tile, 8 waves (2x4), one block per CU.
+template <int WR>
+struct BigTile {
+  static constexpr int BM = 128 * WR, NW = 4 * WR;
+  static constexpr int STAGE = (BM + GBN) * GBK;   // 24 / 32 KiB
+  static constexpr int AP = BM * GBK / 1024 / NW;  // A pieces per wave per stage (2)
+  static constexpr int BP = GBN * GBK / 1024 / NW; // B pieces per wave per stage (4 / 2)
+  static constexpr int PW = AP + BP;               // glds per wave per stage (6 / 4)
+  static constexpr int RP = 64 / WR;               // epilogue rows per pass and wave
+};
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int EPI, bool I32>
-__global__ void __launch_bounds__(256, 2)
+template <int EPI, bool I32, int WR>
+__global__ void __launch_bounds__(256 * WR, 3 - WR)
 k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
             int tiles_m, int tiles_n, Epi e) {
+  using C = BigTile<WR>;
+  constexpr int GBM = C::BM, GAP = C::AP, GBP = C::BP, GSTAGE = C::STAGE, RP = C::RP;
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int nwg = tiles_m * tiles_n;
   int wg = blockIdx.x;
@@ -422,7 +433,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   const int tm = wg / tiles_n, tn = wg % tiles_n;
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave;  // waves side by side along N
+  const int wm = wave >> 2, wn = wave & 3;  // 1 or 2 wave rows of 4 waves along N
 
   // this lane's source row / chunk for each of its A and B pieces (1 KiB = 16 rows)
   const int prow = lane >> 2, ppos = lane & 3;
@@ -466,9 +477,11 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + GST - 1 < nk) {
       issue(kt + GST - 1);
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 stages after kt in flight
+      if constexpr (WR == 1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 stages after kt in flight
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else if (kt + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if constexpr (WR == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -480,7 +493,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     for (int s = 0; s < 2; ++s) {
       v4i fa[4], fb[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const v4i*>(sa + swz64(i * 32 + r32, 2 * s + half));
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const v4i*>(sa + swz64(wm * 128 + i * 32 + r32, 2 * s + half));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         fb[j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * s + half));
@@ -496,35 +509,36 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   }
 
   // ---- epilogue, staged through LDS (the ring is free after the last barrier): each
-  // wave owns a 64 x 72-int32 slice; two passes of 64 rows.  Read back row-major, a lane
-  // takes 4 consecutive columns of one row, so bias / column terms are per lane and the
-  // outputs leave as 4-byte (int8) or 16-byte (f32) stores.
-  int32_t* stg = reinterpret_cast<int32_t*>(lds) + wave * (64 * 72);
+  // wave owns an RP x 72-int32 slice (72 KiB in all); 128 / RP passes of RP rows.  Read
+  // back row-major, a lane takes 4 consecutive columns of one row, so bias / column
+  // terms are per lane and the outputs leave as 4-byte (int8) or 16-byte (f32) stores.
+  int32_t* stg = reinterpret_cast<int32_t*>(lds) + wave * (RP * 72);
+  const int mw = m0 + wm * 128;
   const int c4 = (lane & 15) * 4;
   const int gn0 = n0 + wn * 64 + c4;
   const bool cok = gn0 < N;  // N % 4 == 0 (host-checked): the 4 columns are valid together
   EpiCol4 cc = epi_col4<EPI>(e, gn0, cok);
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = 0; pass < 128 / RP; ++pass) {
     // residual rows of this pass in flight while the tile is staged
-    float4 rv[16];
+    float4 rv[RP / 4];
     if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int gm = min(m0 + pass * 64 + it * 4 + (lane >> 4), M - 1);
+      for (int it = 0; it < RP / 4; ++it) {
+        const int gm = min(mw + pass * RP + it * 4 + (lane >> 4), M - 1);
         rv[it] = cok ? *reinterpret_cast<const float4*>(e.resid + (int64_t)gm * N + gn0) : make_float4(0, 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
+    for (int ii = 0; ii < RP / 32; ++ii)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          stg[(ii * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 72 + j * 32 + r32] = acc[2 * pass + ii][j][r];
+          stg[(ii * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 72 + j * 32 + r32] = acc[pass * (RP / 32) + ii][j][r];
     wave_lds_sync();
     // image / token of this lane's row, advanced incrementally (4 rows per step)
-    int gm = m0 + pass * 64 + (lane >> 4);
+    int gm = mw + pass * RP + (lane >> 4);
     int img = 0, t = 0;
     if constexpr (EPI == EPI_QKV) {
       img = gm / e.tokens;
@@ -542,10 +556,10 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     };
     if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-      for (int it = 0; it < 16; ++it) row_step(it, rv[it]);
+      for (int it = 0; it < RP / 4; ++it) row_step(it, rv[it]);
     } else {
 #pragma unroll 2
-      for (int it = 0; it < 16; ++it) row_step(it, make_float4(0, 0, 0, 0));
+      for (int it = 0; it < RP / 4; ++it) row_step(it, make_float4(0, 0, 0, 0));
     }
     wave_lds_sync();
   }
@@ -726,6 +740,16 @@ k_transpose_pad(const int8_t* __restrict__ src, int8_t* __restrict__ dst, int64_
 
 using namespace nqk;
 
+// projection tile: NQK_BIG_TILE=256 selects the 256x256 / 8-wave variant (read once)
+static int big_tile_rows() {
+  static int wr = 0;
+  if (!wr) {
+    const char* v = getenv("NQK_BIG_TILE");
+    wr = (v && atoi(v) == 256) ? 2 : 1;
+  }
+  return wr;
+}
+
 static Epi make_epi(const nqk_epilogue* p) {
   Epi e{};
   e.zp_flags = p->zp_flags;
@@ -783,14 +807,25 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   auto al = [](const void* q, uintptr_t n) { return q == nullptr || (((uintptr_t)q) & (n - 1)) == 0; };
   const bool aligned = (epi == EPI_RESID) ? (al(params->out[0], 16) && al(params->resid, 16))
                                           : (al(params->out[0], 4) && al(params->out[1], 4) && al(params->out[2], 4));
-  if (big && aligned) {
-    const int tm = (int)((M + GBM - 1) / GBM), tn = (int)((N + GBN - 1) / GBN);
-    const size_t shm = (size_t)GST * GSTAGE;
-    switch (epi) {
-#define LB(E) case E: if (i32) hipLaunchKernelGGL((k_qgemm_big<E, true>), dim3(tm * tn), dim3(256), shm, stream(), a, bt, \
-                                  (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); \
-                       else hipLaunchKernelGGL((k_qgemm_big<E, false>), dim3(tm * tn), dim3(256), shm, stream(), a, bt, \
-                                  (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break;
+  auto normal = [](float x) { return __builtin_fabsf(x) >= 0x1p-100f && __builtin_fabsf(x) <= 0x1p100f; };
+  bool scales_ok = normal(params->s_out[0]) || epi == EPI_RESID || epi == EPI_NULL;
+  if (epi == EPI_QKV) scales_ok = normal(params->s_out[0]) && normal(params->s_out[1]) && normal(params->s_out[2]);
+  if (epi == EPI_GELU) scales_ok = scales_ok && normal(params->div);
+  if (big && aligned && scales_ok) {
+    const int wr = big_tile_rows();
+    const int bm = 128 * wr;
+    const int tm = (int)((M + bm - 1) / bm), tn = (int)((N + GBN - 1) / GBN);
+    const size_t shm = (size_t)GST * (wr == 1 ? BigTile<1>::STAGE : BigTile<2>::STAGE);
+    switch (epi * 4 + (i32 ? 2 : 0) + (wr - 1)) {
+#define LB(E) \
+      case E * 4 + 0: hipLaunchKernelGGL((k_qgemm_big<E, false, 1>), dim3(tm * tn), dim3(256), shm, stream(), a, bt, \
+                                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break; \
+      case E * 4 + 1: hipLaunchKernelGGL((k_qgemm_big<E, false, 2>), dim3(tm * tn), dim3(512), shm, stream(), a, bt, \
+                                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break; \
+      case E * 4 + 2: hipLaunchKernelGGL((k_qgemm_big<E, true, 1>), dim3(tm * tn), dim3(256), shm, stream(), a, bt, \
+                                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break; \
+      case E * 4 + 3: hipLaunchKernelGGL((k_qgemm_big<E, true, 2>), dim3(tm * tn), dim3(512), shm, stream(), a, bt, \
+                                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break;
       LB(EPI_QKV) LB(EPI_RESID) LB(EPI_GELU) LB(EPI_NULL)
 #undef LB
       default: break;

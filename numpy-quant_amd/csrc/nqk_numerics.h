@@ -7,8 +7,27 @@
 namespace nqk {
 namespace {
 
+// ------------------------------------------------------------------ division
+// a / b: FAST = v_rcp_f32 estimate + one residual correction (4 VALU instead of the ~10
+// of the IEEE sequence).  It is NOT correctly rounded for every (a, b); it is used only
+// inside np_expf_t / ref_erf_t, where nqk_selftest_fastmath proves on the GPU, over all
+// 2^32 float inputs, that the fast and the IEEE variants of the two functions return
+// identical bits (tests/test_gpu_kernels.py::test_fast_division_exp_erf_exhaustive).
+template <bool FAST>
+__device__ __forceinline__ float div_t(float a, float b) {
+  if constexpr (FAST) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    const float q = a * r;
+    const float e = __builtin_fmaf(-b, q, a);
+    return __builtin_fmaf(e, r, q);
+  } else {
+    return a / b;
+  }
+}
+
 // ------------------------------------------------------------------ numpy float32 exp
-__device__ __forceinline__ float np_expf(float x) {
+template <bool FAST>
+__device__ __forceinline__ float np_expf_t(float x) {
   const float xmax = 88.72283935546875f, xmin = -103.97208404541015625f;
   const bool over = x >= xmax, under = x <= xmin;
   float xx = (over || under) ? 0.0f : x;
@@ -25,26 +44,33 @@ __device__ __forceinline__ float np_expf(float x) {
   num = __builtin_fmaf(num, r, 9.999999999980870924916e-01f);
   float den = __builtin_fmaf(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
   den = __builtin_fmaf(den, r, 1.0f);
-  float poly = num / den;
+  float poly = div_t<FAST>(num, den);
   poly = __builtin_ldexpf(poly, (int)q);
   poly = over ? __builtin_inff() : poly;
   poly = under ? 0.0f : poly;
   return x != x ? x : poly;  // NaN passes through (selects, no branch)
 }
 
+// the fast-division variant everywhere: bit-identical on all 2^32 inputs (see div_t)
+__device__ __forceinline__ float np_expf(float x) { return np_expf_t<true>(x); }
+
 // numpy_helper.py:95-112 (A&S 7.1.26), float32 throughout
-__device__ __forceinline__ float ref_erf(float x) {
+template <bool FAST>
+__device__ __forceinline__ float ref_erf_t(float x) {
   float sgn = (x > 0.0f) ? 1.0f : ((x < 0.0f) ? -1.0f : (x == 0.0f ? 0.0f : x));
   float ax = __builtin_fabsf(x);
-  float t = 1.0f / (1.0f + 0.3275911f * ax);
+  const float den = 1.0f + 0.3275911f * ax;
+  // FAST: 1 / inf must stay 0 (the residual step would make it NaN)
+  float t = FAST ? (den == __builtin_inff() ? 0.0f : div_t<true>(1.0f, den)) : 1.0f / den;
   float p = 1.061405429f * t + -1.453152027f;
   p = p * t;
   p = p + 1.421413741f;
   p = p * t + -0.284496736f;
   p = p * t + 0.254829592f;
-  float y = 1.0f - p * t * np_expf(-ax * ax);
+  float y = 1.0f - p * t * np_expf_t<FAST>(-ax * ax);
   return sgn * y;
 }
+__device__ __forceinline__ float ref_erf(float x) { return ref_erf_t<true>(x); }
 
 // ------------------------------------------------------------------ NumPy pairwise sum
 // The recursion of NumPy's pairwise_sum (n < 8: sequential; n <= 128: 8 interleaved

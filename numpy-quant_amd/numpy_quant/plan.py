@@ -27,6 +27,8 @@ from .tensor import FTensor, QTensor
 
 EPI_QKV, EPI_SCORES, EPI_PV, EPI_RESID, EPI_GELU = 0, 1, 2, 3, 4
 
+_EPI_NAMES = {EPI_QKV: "qkv", EPI_SCORES: "scores", EPI_PV: "pv", EPI_RESID: "resid", EPI_GELU: "gelu"}
+
 # module switch: the one-kernel attention (nqk_attention_fused) where it applies
 FUSED_ATTENTION = True
 
@@ -332,8 +334,7 @@ class FusedLayer:
         w = ws.get(B, T, Tp, H, Dh, D, F, unfused_attention=not self.attn_fused)
         call = _lib.call
         # 1) LN1 + quantize (LN1 output feeds the Q/K/V MatMuls)
-        call("nqk_ln_quant", x.dev.vp, self.g1.vp, self.be1.vp, w["lnq"].vp, Mrows, D, self.eps1,
-             _f32(self.p_ln1.scale), _zp(self.p_ln1), bw)
+        _ln_quant(x.dev, self.g1, self.be1, w["lnq"], Mrows, D, self.eps1, self.p_ln1, bw)
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D, col=self.col_qkv.ptr,
@@ -355,7 +356,7 @@ class FusedLayer:
             t0 = KM.TIMER.begin() if KM.TIMER is not None else None
             call("nqk_attention_fused", w["q"].vp, w["k"].vp, w["v"].vp, w["ctx"].vp, B * H, ctypes.byref(a))
             if t0 is not None:
-                KM.TIMER.end("attention_fused", t0, (2 * 2 * B * H * T * T * Dh, 3 * B * H * T * Dh + B * T * D))
+                KM.TIMER.end("attention", t0, (2 * 2 * B * H * T * T * Dh, 3 * B * H * T * Dh + B * T * D))
         else:
             self._attention_unfused(w, B, T, Tp, H, Dh, D)
         # 7) output projection + bias + residual
@@ -365,8 +366,7 @@ class FusedLayer:
                       resid=x.dev.ptr, out=[x1.ptr])
         _gemm(EPI_RESID, w["ctx"], self.bt_o, 1, Mrows, D, D, D, D, None, 0, 0, e)
         # 8) LN2 + quantize
-        call("nqk_ln_quant", x1.vp, self.g2.vp, self.be2.vp, w["ln2q"].vp, Mrows, D, self.eps2,
-             _f32(self.p_ln2.scale), _zp(self.p_ln2), bw)
+        _ln_quant(x1, self.g2, self.be2, w["ln2q"], Mrows, D, self.eps2, self.p_ln2, bw)
         # 9) FFN up + bias + GELU + quantize
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr,
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
@@ -380,6 +380,13 @@ class FusedLayer:
                       resid=x1.ptr, out=[x2.ptr])
         _gemm(EPI_RESID, w["h"], self.bt_2, 1, Mrows, D, F, F, F, None, 0, 0, e)
         m.x_out.data = FTensor(x2)
+
+
+def _ln_quant(x, g, b, out, rows, cols, eps, p, bw):
+    t0 = KM.TIMER.begin() if KM.TIMER is not None else None
+    _lib.call("nqk_ln_quant", x.vp, g.vp, b.vp, out.vp, rows, cols, eps, _f32(p.scale), _zp(p), bw)
+    if t0 is not None:
+        KM.TIMER.end("ln_quant", t0, (0, rows * cols * 5 + 2 * cols * 4))
 
 
 def _cat0(arrs):
@@ -404,7 +411,7 @@ def _gemm(epi, a, bt, batch, M, N, K, lda, ldb, bmap, a_ms, b_ms, e):
     _lib.call("nqk_qgemm_fused", epi, a.vp, bt.vp, batch, M, N, K, lda, ldb,
               _lib.i64arr(bmap) if bmap is not None else None, a_ms, b_ms, ctypes.byref(e))
     if t0 is not None:
-        KM.TIMER.end("qgemm_fused", t0, (2 * batch * M * N * K, batch * (M * K + N * K)))
+        KM.TIMER.end("qgemm_" + _EPI_NAMES[epi], t0, (2 * batch * M * N * K, batch * (M * K + N * K)))
 
 
 class Workspace:

@@ -28,6 +28,21 @@ def test_exp_matches_numpy_on_64M_floats():
         assert same.all(), (x[~same][:5], y[~same][:5], ref[~same][:5])
 
 
+def test_fast_division_exp_erf_exhaustive():
+    """The fused kernels use exp / erf with a 4-instruction division (v_rcp_f32 + one
+    residual correction).  That division is not correctly rounded in general, so the
+    fast functions are used only because they equal the IEEE-division ones bit for bit
+    on every one of the 2^32 float inputs, which this test establishes on the device."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    counts = DeviceArray.from_host(np.zeros(2, np.uint64))
+    ex = DeviceArray.from_host(np.zeros(2, np.uint32))
+    _lib.call("nqk_selftest_fastmath", counts.vp, ex.vp)
+    c, e = counts.to_host(), ex.to_host()
+    assert c[0] == 0, f"fast exp differs on {c[0]} inputs, e.g. {e[0:1].view(np.float32)}"
+    assert c[1] == 0, f"fast erf differs on {c[1]} inputs, e.g. {e[1:2].view(np.float32)}"
+
+
 @pytest.mark.parametrize("rows,cols", [(7, 5), (33, 128), (64, 197), (17, 768), (9, 3072), (3, 1000), (2, 129)])
 def test_pairwise_softmax_layernorm(rows, cols):
     from numpy_quant.tensor import FTensor
