@@ -14,6 +14,8 @@
 //   k_ln_quant        LayerNormalization (NumPy pairwise means) + quantize
 //   k_softmax_quant   Softmax (NumPy exp + pairwise sum) + quantize + row sums
 //   k_transpose_pad   int8 [nb][R][C] -> [nb][C][Rp] zero padded, + row sums
+#include <type_traits>
+
 #include "nqk_common.h"
 #include "nqk_numerics.h"
 
@@ -469,44 +471,66 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
 
+  // one barrier per k-step: after it every wave has finished reading slot (kt-1)%3,
+  // which the same step refills with stage kt+2 (glds spread between the MFMAs).  The
+  // last two steps issue nothing (peeled, so each step body is one basic block).
   const int nk = K / GBK;
-#pragma unroll
-  for (int st = 0; st < GST - 1; ++st)
-    if (st < nk) issue(st);
+  issue(0);
+  if (nk > 1) issue(1);
   const int r32 = lane & 31, half = lane >> 5;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + GST - 1 < nk) {
-      issue(kt + GST - 1);
-      if constexpr (WR == 1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 stages after kt in flight
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else if (kt + 1 < nk) {
-      if constexpr (WR == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  auto kstep = [&](int kt, auto refill, auto drain) {
+    if constexpr (decltype(drain)::value) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else if constexpr (WR == 1) {
+      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");  // stage kt+1 may fly
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     const int8_t* sa = lds + (kt % GST) * GSTAGE;
     const int8_t* sb = sa + GBM * GBK;
+    v4i fa[2][4], fb[2][2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      v4i fa[4], fb[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const v4i*>(sa + swz64(wm * 128 + i * 32 + r32, 2 * s + half));
+      for (int i = 0; i < 4; ++i) fa[s][i] = *reinterpret_cast<const v4i*>(sa + swz64(wm * 128 + i * 32 + r32, 2 * s + half));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        fb[j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * s + half));
+        fb[s][j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * s + half));
+    }
+    if constexpr (decltype(refill)::value) issue(kt + 2);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+    // issue order: the 6 s=0 fragment reads, then the MFMAs with the s=1 reads and the
+    // next stage's glds spread between them
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
+    if constexpr (decltype(refill)::value) {
+#pragma unroll
+      for (int g = 0; g < GAP + GBP; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  for (int kt = 0; kt + 2 < nk; ++kt) kstep(kt, T_{}, F_{});
+  if (nk >= 2) kstep(nk - 2, F_{}, F_{});
+  kstep(nk - 1, F_{}, T_{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
   // ---- epilogue, staged through LDS (the ring is free after the last barrier): each
   // wave owns an RP x 72-int32 slice (72 KiB in all); 128 / RP passes of RP rows.  Read

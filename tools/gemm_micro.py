@@ -75,7 +75,10 @@ for name, (N, K, epi) in shapes.items():
     def null():
         _lib.call("nqk_qgemm_fused", 5, a.vp, bt.vp, 1, M, N, K, K, K, None, 0, 0, ctypes.byref(e))
 
+    only = os.environ.get("GM_ONLY")  # e.g. "down:null_epi" (profiling one variant)
     for tag, fn in (("fused", fused), ("null_epi", null), ("qgemm_i8", plain)):
+        if only and only != f"{name}:{tag}":
+            continue
         ms = timeit(fn)
         print(f"{name:5s} {tag:9s} M={M} N={N} K={K}: {ms * 1e3:8.1f} us  {ops / ms / 1e9:8.1f} TOPS  "
               f"({100 * ops / ms / 1e9 / 5033.2:5.1f}% of int8 peak)", flush=True)
