@@ -228,6 +228,10 @@ int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_t* v, int8_
  * reference's erf (used by the fused kernels) with the IEEE-division ones on all 2^32
  * float inputs; adds the mismatch counts to counts_dev[0] (exp) / [1] (erf). */
 int nqk_selftest_fastmath(unsigned long long* counts_dev, uint32_t* examples_dev);
+/* Diagnostic: checks the error bound of the GELU filter's cheap approximation on all
+ * 2^32 inputs; stats_dev[0] = violations, [1] = an example, [2 + e] = max error per
+ * exponent in units of |h| * 2^-24 (258 entries, zero-initialised by the caller). */
+int nqk_selftest_gelu_filter(unsigned long long* stats_dev);
 
 /* ------------------------------------------------ multi-GPU replicas (RCCL) */
 int nqk_comm_unique_id(void* id128);                         /* rank 0 */

@@ -265,6 +265,29 @@ __global__ void k_fastmath_check(unsigned long long* counts, uint32_t* ex) {
   if (cr) atomicAdd(counts + 1, cr);
 }
 
+// exhaustive check of the GELU filter bound (nqk_numerics.h gelu_fast) for the graph
+// constants div = sqrt2 (as f32), add1 = 1, mul2 = 0.5: st[0] = violations, st[1] = an
+// example input; st[2 + e] = max over inputs with biased exponent e of the error in units
+// of |h| * 2^-24 (diagnostic)
+__global__ void k_gelu_filter_check(unsigned long long* st) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const double rdiv = 1.0 / (double)1.41421354f;
+  unsigned long long bad = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t(1) << 32); i += stride) {
+    const float h = __uint_as_float((uint32_t)i);
+    if (!(__builtin_fabsf(h) < 0x1p64f)) continue;  // NaN, inf and huge |h| take the exact path
+    const float a = gelu_fast(h), b = gelu_ref(h, rdiv, 1.0f, 0.5f);
+    const float d = __builtin_fabsf(a - b);
+    const bool ok = (double)d <= (double)GELU_REL * __builtin_fabs((double)h) + (double)GELU_ABS;
+    if (!ok) { ++bad; st[1] = i; }
+    const int ex = (int)((i >> 23) & 0xff);
+    const double units = __builtin_fabs((double)h) > 0 ? (double)d / (__builtin_fabs((double)h) * 0x1p-24) : 0.0;
+    const unsigned long long u = (unsigned long long)(units < 1e18 ? units : 1e18);
+    if (u) atomicMax(st + 2 + ex, u);
+  }
+  if (bad) atomicAdd(st, bad);
+}
+
 // drop extent-1 dimensions and merge neighbours that are contiguous for every operand
 // (the output / destination index is always row-major), then precompute magic divisors
 Nd make_nd(int ndim, const int64_t* shape, const int64_t* s0, const int64_t* s1, const int64_t* s2) {
@@ -333,6 +356,11 @@ extern "C" int nqk_binary_f32(int op, const float* a, const float* b, float* out
 extern "C" int nqk_selftest_fastmath(unsigned long long* counts_dev, uint32_t* examples_dev) {
   hipLaunchKernelGGL(k_fastmath_check, dim3(256 * 64), dim3(256), 0, stream(), counts_dev, examples_dev);
   return launch_status("nqk_selftest_fastmath");
+}
+
+extern "C" int nqk_selftest_gelu_filter(unsigned long long* stats_dev) {
+  hipLaunchKernelGGL(k_gelu_filter_check, dim3(256 * 64), dim3(256), 0, stream(), stats_dev);
+  return launch_status("nqk_selftest_gelu_filter");
 }
 
 extern "C" int nqk_unary_f32(int op, const float* x, float* out, int64_t n) {

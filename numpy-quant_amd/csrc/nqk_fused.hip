@@ -73,6 +73,8 @@ struct Epi {
   float add1, mul2;      // EPI_GELU: + 1.0, * 0.5
   int tokens, heads, hdim, ld_out;
   double lo, hi;
+  int gelu_filter;        // EPI_GELU: constants are the ViT GELU's (sqrt2, 1, 0.5)
+  float rsf, zpf, lof, hif;  // f32 RN(1/s_out), zp_out[0], lo, hi for the filter
 };
 
 enum { EPI_QKV = 0, EPI_SCORES = 1, EPI_PV = 2, EPI_RESID = 3, EPI_GELU = 4, EPI_NULL = 5 };
@@ -225,18 +227,57 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
     if (a[0] == (int32_t)0x80000001) ((int32_t*)e.out[0])[0] = (int)d[1];
   } else {
     uint32_t packed = 0;
+    if constexpr (EPI == EPI_GELU) {
+      if (e.gelu_filter) {
+        // filter: gelu_fast is within GELU_REL*|h| + GELU_ABS of the exact chain (checked
+        // on all 2^32 inputs); where that error, the rounding of t = y / s and of zp + t
+        // cannot reach a rounding boundary, rint(zp + t) is decided by the cheap value.
+        // Everything else (and NaN / huge h) takes the exact chain in a uniform branch.
+        float h[4];
+        int q[4];
+        bool slow[4], any_slow = false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      int q;
-      if constexpr (EPI == EPI_GELU) {
-        const float h = c.bias[k] + d[k];
-        const float aa = ref_erf(div_rc_u(h, e.div, e.rdiv)) + e.add1;
-        const float y = (h * aa) * e.mul2;
-        q = quant_zp_u(y, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
-      } else {  // EPI_QKV
-        q = quant_zp_u(c.bias[k] + d[k], c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+        for (int k = 0; k < 4; ++k) {
+          h[k] = c.bias[k] + d[k];
+          const float ah = __builtin_fabsf(h[k]);
+          const float tf = gelu_fast(h[k]) * e.rsf;
+          const float u = e.zpf + tf;
+          const float r = __builtin_rintf(u);
+          const float dist = __builtin_fabsf(u - r);
+          const float err = ((GELU_REL * ah + GELU_ABS) * e.rsf * 1.01f + __builtin_fabsf(tf) * 0x1p-20f +
+                             __builtin_fabsf(u) * 0x1p-22f) + 0x1p-100f;
+          const bool inner = (0.5f - dist) > err && err < 0.25f;
+          const bool outside = err < 0.5f && (u - err > e.hif + 0.5f || u + err < e.lof - 0.5f);
+          slow[k] = !(ah < 0x1p64f && (inner || outside));
+          any_slow |= slow[k];
+          const float rc = __builtin_fminf(__builtin_fmaxf(r, e.lof), e.hif);
+          q[k] = (int)rc;
+        }
+        if (__builtin_expect(__any(any_slow), 0)) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (slow[k]) {
+              const float aa = ref_erf(div_rc_u(h[k], e.div, e.rdiv)) + e.add1;
+              q[k] = quant_zp_u((h[k] * aa) * e.mul2, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) packed |= ((uint32_t)(q[k] & 0xff)) << (8 * k);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float h = c.bias[k] + d[k];
+          const float aa = ref_erf(div_rc_u(h, e.div, e.rdiv)) + e.add1;
+          const int q = quant_zp_u((h * aa) * e.mul2, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+          packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+        }
       }
-      packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+    } else {  // EPI_QKV
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = quant_zp_u(c.bias[k] + d[k], c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+        packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+      }
     }
     if constexpr (EPI == EPI_GELU) {
       *reinterpret_cast<uint32_t*>(c.out + (int64_t)gm * N + c.dd) = packed;
@@ -801,6 +842,14 @@ static Epi make_epi(const nqk_epilogue* p) {
   e.ld_out = p->ld_out;
   e.lo = -__builtin_ldexp(1.0, p->bit_width - 1);
   e.hi = __builtin_ldexp(1.0, p->bit_width - 1) - 1.0;
+  // the GELU filter's bound is proven for these constants only (nqk_selftest_gelu_filter)
+  e.gelu_filter = p->div == 1.41421354f && p->add1 == 1.0f && p->mul2 == 0.5f && p->zp_out[0] >= -(1 << 20) &&
+                  p->zp_out[0] <= (1 << 20) && __builtin_fabsf(p->s_out[0]) >= 0x1p-60f &&
+                  __builtin_fabsf(p->s_out[0]) <= 0x1p60f && !(getenv("NQK_NO_GELU_FILTER"));
+  e.rsf = (float)(1.0 / (double)p->s_out[0]);
+  e.zpf = (float)p->zp_out[0];
+  e.lof = (float)e.lo;
+  e.hif = (float)e.hi;
   return e;
 }
 

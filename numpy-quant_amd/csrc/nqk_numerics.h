@@ -72,6 +72,32 @@ __device__ __forceinline__ float ref_erf_t(float x) {
 }
 __device__ __forceinline__ float ref_erf(float x) { return ref_erf_t<true>(x); }
 
+// ------------------------------------------------------------------ GELU filter
+// The FFN chain of the ViT graphs, h -> (h * (erf(h / sqrt2) + 1)) * 0.5 (model.py Div,
+// Erf, Add, Mul, Mul on f32; numpy_helper.py:95-112 erf), as the fused kernels run it:
+__device__ __forceinline__ float gelu_ref(float h, double rdiv, float add1, float mul2) {
+  const float a = ref_erf((float)((double)h * rdiv)) + add1;
+  return (h * a) * mul2;
+}
+// and a cheap approximation of it (hardware rcp / exp2).  nqk_selftest_gelu_filter
+// checks on the GPU, for every one of the 2^32 f32 inputs with |h| < 2^64, that
+// |gelu_fast(h) - gelu_ref(h)| <= GELU_REL * |h| + GELU_ABS; the GEMM epilogue only
+// trusts gelu_fast where that bound cannot move the quantized value (nqk_fused.hip).
+constexpr float GELU_REL = 0x1p-20f, GELU_ABS = 0x1p-60f;
+__device__ __forceinline__ float gelu_fast(float h) {
+  const float x = h * 0.70710677f;
+  const float ax = __builtin_fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, ax, 1.0f));
+  float p = __builtin_fmaf(1.061405429f, t, -1.453152027f);
+  p = __builtin_fmaf(p, t, 1.421413741f);
+  p = __builtin_fmaf(p, t, -0.284496736f);
+  p = __builtin_fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-(ax * ax) * 1.44269504f);
+  const float y = __builtin_fmaf(-(p * t), e, 1.0f);
+  const float erf = __builtin_copysignf(y, x);
+  return (h * (erf + 1.0f)) * 0.5f;
+}
+
 // ------------------------------------------------------------------ NumPy pairwise sum
 // The recursion of NumPy's pairwise_sum (n < 8: sequential; n <= 128: 8 interleaved
 // accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the n % 8 tail;

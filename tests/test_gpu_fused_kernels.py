@@ -36,3 +36,36 @@ def test_ln_quant(rows, cols, bw, zp):
     out = DeviceArray((rows, cols), np.int8)
     _lib.call("nqk_ln_quant", dx.vp, dg.vp, db.vp, out.vp, rows, cols, float(eps), float(s), zp, bw)
     np.testing.assert_array_equal(out.to_host().astype(np.int64), ref)
+
+
+@pytest.mark.parametrize("s_out,zp,bw", [(0.041, -7, 8), (0.0023, 0, 8), (0.31, -3, 4), (1e-5, 100, 8)])
+def test_gelu_epilogue_filter_matches_exact_chain(s_out, zp, bw, monkeypatch):
+    """FFN-up GEMM with the GELU epilogue (model.py MatMul -> Add -> Div -> Erf -> Add ->
+    Mul -> Mul -> quantize): the filtered epilogue (cheap GELU where its proven error
+    bound cannot change the rounding, exact chain elsewhere) equals the exact chain
+    everywhere.  Small output scales put many values next to rounding boundaries."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_GELU, _gemm
+    rng = np.random.default_rng(int(s_out * 1e6) + bw)
+    M, N, K = 1024 + 77, 3072, 768
+    a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
+    bt_h = rng.integers(-20, 21, size=(N, K), dtype=np.int8)
+    bt = DeviceArray.from_host(bt_h)
+    col = DeviceArray.from_host(bt_h.astype(np.int64).sum(axis=1))
+    bias = DeviceArray.from_host((0.02 * rng.standard_normal(N)).astype(np.float32))
+    outs = []
+    for flag in (None, "1"):
+        if flag:
+            monkeypatch.setenv("NQK_NO_GELU_FILTER", flag)
+        out = DeviceArray((M, N), np.int8)
+        e = _lib.Epilogue()
+        e.zp_flags, e.bit_width, e.group_cols = _lib.ZP_COL, bw, 1 << 30
+        e.zpa, e.col = 5, col.ptr
+        e.s_acc[0] = float(np.float32(1.3e-4))
+        e.s_out[0], e.zp_out[0], e.out[0] = s_out, zp, out.ptr
+        e.bias = bias.ptr
+        e.div, e.add1, e.mul2 = float(np.float32(1.4142135381698608)), 1.0, 0.5
+        _gemm(EPI_GELU, a, bt, 1, M, N, K, K, K, None, 0, 0, e)
+        outs.append(out.to_host())
+    np.testing.assert_array_equal(outs[0], outs[1])

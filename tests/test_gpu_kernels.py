@@ -43,6 +43,21 @@ def test_fast_division_exp_erf_exhaustive():
     assert c[1] == 0, f"fast erf differs on {c[1]} inputs, e.g. {e[1:2].view(np.float32)}"
 
 
+def test_gelu_filter_bound_exhaustive():
+    """The GELU epilogue computes a cheap approximation first and falls back to the
+    exact chain wherever the approximation's error bound could change the quantized
+    value.  This test proves the bound |fast - exact| <= 2^-20 |h| + 2^-60 on every
+    f32 input with |h| < 2^64 (the others always take the exact chain)."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    st = DeviceArray.from_host(np.zeros(258, np.uint64))
+    _lib.call("nqk_selftest_gelu_filter", st.vp)
+    s = st.to_host()
+    worst = {e - 127: int(v) for e, v in enumerate(s[2:]) if v}
+    print("max error per exponent (units of |h| 2^-24):", worst)
+    assert s[0] == 0, f"{s[0]} inputs exceed the bound, e.g. h = {np.uint32(s[1]).view(np.float32)}"
+
+
 @pytest.mark.parametrize("rows,cols", [(7, 5), (33, 128), (64, 197), (17, 768), (9, 3072), (3, 1000), (2, 129)])
 def test_pairwise_softmax_layernorm(rows, cols):
     from numpy_quant.tensor import FTensor
