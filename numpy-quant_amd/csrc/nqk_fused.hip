@@ -73,8 +73,9 @@ struct Epi {
   float add1, mul2;      // EPI_GELU: + 1.0, * 0.5
   int tokens, heads, hdim, ld_out;
   double lo, hi;
-  int gelu_filter;        // EPI_GELU: constants are the ViT GELU's (sqrt2, 1, 0.5)
+  int gelu_filter;           // EPI_GELU: constants are the ViT GELU's (sqrt2, 1, 0.5)
   float rsf, zpf, lof, hif;  // f32 RN(1/s_out), zp_out[0], lo, hi for the filter
+  float g_rel, g_abs;        // filter error terms, in units of t
 };
 
 enum { EPI_QKV = 0, EPI_SCORES = 1, EPI_PV = 2, EPI_RESID = 3, EPI_GELU = 4, EPI_NULL = 5 };
@@ -204,17 +205,21 @@ __device__ __forceinline__ int quant_zp_u(float x, float s, double rs, double zp
   return (int)__builtin_rint(__builtin_fmin(__builtin_fmax(u, lo), hi));
 }
 
+// dequantize one accumulator: f32( f64(acc - zero-point term) * f64(s) )
+template <bool I32>
+__device__ __forceinline__ float dequant_elem(int32_t acc, int64_t colterm, float s_acc) {
+  double vd;
+  if constexpr (I32) vd = (double)(acc - (int32_t)colterm);
+  else vd = (double)((int64_t)acc - colterm);
+  return (float)(vd * (double)s_acc);
+}
+
 template <int EPI, bool I32>
 __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, int N, const EpiCol4& c, v4i a,
                                          float4 r) {
   float d[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    double vd;
-    if constexpr (I32) vd = (double)(a[k] - (int32_t)c.colterm[k]);
-    else vd = (double)((int64_t)a[k] - c.colterm[k]);
-    d[k] = (float)(vd * (double)c.s_acc);
-  }
+  for (int k = 0; k < 4; ++k) d[k] = (EPI == EPI_GELU) ? 0.0f : dequant_elem<I32>(a[k], c.colterm[k], c.s_acc);
   if constexpr (EPI == EPI_RESID) {
     const int64_t o = (int64_t)gm * N + c.dd;
     float4 y;
@@ -230,35 +235,37 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
     if constexpr (EPI == EPI_GELU) {
       if (e.gelu_filter) {
         // filter: gelu_fast is within GELU_REL*|h| + GELU_ABS of the exact chain (checked
-        // on all 2^32 inputs); where that error, the rounding of t = y / s and of zp + t
-        // cannot reach a rounding boundary, rint(zp + t) is decided by the cheap value.
-        // Everything else (and NaN / huge h) takes the exact chain in a uniform branch.
-        float h[4];
+        // on all 2^32 inputs); h comes from an f32 dequant, which equals the f64 one for
+        // |v| < 2^24 (v and s_acc exact in f32, one rounding); t = y / s from an f32
+        // product (within |t| 2^-22.9 of RN32(y / s)).  Where those errors cannot reach a
+        // rounding boundary of t (zp is an integer, so zp + t rounds like t away from
+        // ties), rint(zp + t) is decided by the cheap value; all other elements (|v| >=
+        // 2^24, NaN, |h| >= 2^64) take the exact chain in a wave-uniform branch.
         int q[4];
         bool slow[4], any_slow = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          h[k] = c.bias[k] + d[k];
-          const float ah = __builtin_fabsf(h[k]);
-          const float tf = gelu_fast(h[k]) * e.rsf;
-          const float u = e.zpf + tf;
-          const float r = __builtin_rintf(u);
-          const float dist = __builtin_fabsf(u - r);
-          const float err = ((GELU_REL * ah + GELU_ABS) * e.rsf * 1.01f + __builtin_fabsf(tf) * 0x1p-20f +
-                             __builtin_fabsf(u) * 0x1p-22f) + 0x1p-100f;
-          const bool inner = (0.5f - dist) > err && err < 0.25f;
-          const bool outside = err < 0.5f && (u - err > e.hif + 0.5f || u + err < e.lof - 0.5f);
-          slow[k] = !(ah < 0x1p64f && (inner || outside));
+          int32_t vi;
+          if constexpr (I32) vi = a[k] - (int32_t)c.colterm[k];
+          else vi = (int32_t)__builtin_fmin(__builtin_fmax((double)((int64_t)a[k] - c.colterm[k]), -2147483520.0), 2147483520.0);
+          const float df = (float)vi * c.s_acc;
+          const float hf = c.bias[k] + df;
+          const float tf = gelu_fast(hf) * e.rsf;
+          const float r = __builtin_rintf(tf);
+          const float room = 0.5f - __builtin_fabsf(tf - r);
+          const float err = __builtin_fmaf(__builtin_fabsf(hf), e.g_rel, e.g_abs) + __builtin_fabsf(tf) * 0x1p-22f;
+          slow[k] = !((room > err) & (err < 0.25f) & (__builtin_fabsf(hf) < 0x1p64f) &
+                      (vi < (1 << 24)) & (vi > -(1 << 24)));
           any_slow |= slow[k];
-          const float rc = __builtin_fminf(__builtin_fmaxf(r, e.lof), e.hif);
-          q[k] = (int)rc;
+          q[k] = (int)__builtin_fminf(__builtin_fmaxf(r + e.zpf, e.lof), e.hif);
         }
         if (__builtin_expect(__any(any_slow), 0)) {
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (slow[k]) {
-              const float aa = ref_erf(div_rc_u(h[k], e.div, e.rdiv)) + e.add1;
-              q[k] = quant_zp_u((h[k] * aa) * e.mul2, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+              const float h = c.bias[k] + dequant_elem<I32>(a[k], c.colterm[k], c.s_acc);
+              const float aa = ref_erf(div_rc_u(h, e.div, e.rdiv)) + e.add1;
+              q[k] = quant_zp_u((h * aa) * e.mul2, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
             }
         }
 #pragma unroll
@@ -266,7 +273,7 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float h = c.bias[k] + d[k];
+          const float h = c.bias[k] + dequant_elem<I32>(a[k], c.colterm[k], c.s_acc);
           const float aa = ref_erf(div_rc_u(h, e.div, e.rdiv)) + e.add1;
           const int q = quant_zp_u((h * aa) * e.mul2, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
           packed |= ((uint32_t)(q & 0xff)) << (8 * k);
@@ -847,6 +854,10 @@ static Epi make_epi(const nqk_epilogue* p) {
                   p->zp_out[0] <= (1 << 20) && __builtin_fabsf(p->s_out[0]) >= 0x1p-60f &&
                   __builtin_fabsf(p->s_out[0]) <= 0x1p60f && !(getenv("NQK_NO_GELU_FILTER"));
   e.rsf = (float)(1.0 / (double)p->s_out[0]);
+  // |d(gelu)/dh| <= 1.13, so an h error of |d| 2^-23 moves y by at most |d| 2^-22.8
+  const double ars = __builtin_fabs(1.0 / (double)p->s_out[0]) * 1.02;
+  e.g_rel = (float)(GELU_REL * ars);
+  e.g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
   e.zpf = (float)p->zp_out[0];
   e.lof = (float)e.lo;
   e.hif = (float)e.hi;
