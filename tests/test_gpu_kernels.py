@@ -156,3 +156,20 @@ def test_quantize_rowsum_and_graph_capture():
     _lib.call("nqk_graph_launch", g)
     np.testing.assert_array_equal(out.to_host().astype(np.int64), ref)
     _lib.call("nqk_graph_destroy", g)
+
+
+@pytest.mark.parametrize("batch,M,N,K", [(1, 50176 // 8, 768, 768), (1, 197, 768, 768), (3, 130, 257, 1000),
+                                         (2, 256, 200, 386), (1, 129, 131, 2)])
+def test_sgemm_mfma_equals_fma_chain_kernel(batch, M, N, K, monkeypatch):
+    """v_mfma_f32_32x32x2_f32 path vs the VALU fmaf-chain kernel (both in the BLAS K
+    blocking, nqk_sgemm): bit-identical, including batched and ragged tiles."""
+    from numpy_quant import kernels as KM
+    from numpy_quant.device import DeviceArray
+    rng = np.random.default_rng(M * N + K)
+    a = DeviceArray.from_host(rng.standard_normal((batch, M, K), dtype=np.float32))
+    b = DeviceArray.from_host(rng.standard_normal((batch, K, N), dtype=np.float32))
+    bmap = [1, 1, 0, 1, 0]
+    got = KM.sgemm(a, K, 1, b, N, 1, M, N, K, batch=batch, bmap=bmap, a_ms=M * K, b_ms=K * N).to_host()
+    monkeypatch.setenv("NQK_SGEMM_VALU", "1")
+    ref = KM.sgemm(a, K, 1, b, N, 1, M, N, K, batch=batch, bmap=bmap, a_ms=M * K, b_ms=K * N).to_host()
+    np.testing.assert_array_equal(got, ref)
