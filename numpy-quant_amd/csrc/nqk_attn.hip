@@ -31,7 +31,18 @@ struct AttnArgs {
   int kq, kp;          // zq*zk*64, zp*zv*T
   float s_qk, div, s_p, s_pv, s_ctx;
   double rdiv, rs_p, zp_p, rs_ctx, zp_ctx, lo, hi;
+  float inv_div, rs_ctx_f, zp_p_f, zp_ctx_f, lo_f, hi_f;  // FAST path constants
 };
+
+// rint(zp + t) for t approximated by tf with |t - tf| <= |tf| * 2^-21: decided by tf when
+// the boundary is farther than that (zp is an integer, so zp + t rounds like t away from
+// ties); else *slow is set and the caller recomputes exactly
+__device__ __forceinline__ int quant_filter(float tf, float zpf, float lof, float hif, bool* slow) {
+  const float r = __builtin_rintf(tf);
+  const float room = 0.5f - __builtin_fabsf(tf - r);
+  *slow = !(room > __builtin_fabsf(tf) * 0x1p-21f + 0x1p-126f);
+  return (int)__builtin_fminf(__builtin_fmaxf(r + zpf, lof), hif);
+}
 
 __device__ __forceinline__ int swz64a(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
@@ -73,7 +84,11 @@ __device__ __forceinline__ float xor32f(float x) { return __int_as_float(xor32i(
 // quantize are all in-lane; one cross-half exchange combines them.  The context is
 // computed transposed as well (O^T = V^T P^T), so each lane stores 4 consecutive
 // head dimensions of its query row at once.
-template <int NT, int TC>  // TC: compile-time token count (0: runtime a.T)
+// FAST: the dequantized scores / context are formed in f32 (exact: every |acc - term| <
+// 2^24, host-checked), the scores Div is a power of two (an exact f32 multiply), and the
+// P / context quantizations go through a rounding filter (t from one f32 product, exact
+// chain for any element within the product's error bound of a rounding boundary).
+template <int NT, int TC, bool FAST>  // TC: compile-time token count (0: runtime a.T)
 __global__ void __launch_bounds__(256, 2)
 k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int8_t* __restrict__ Vg,
             int8_t* __restrict__ ctx, AttnArgs a) {
@@ -164,9 +179,11 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * qq + j, n = c * 32 + 8 * qq + 4 * h + j;
           const int vv = acc[c][r] - rowterm - ck[j];
-          const float d = (float)((double)vv * (double)a.s_qk);
+          float y;
+          if constexpr (FAST) y = ((float)vv * a.s_qk) * a.inv_div;
+          else y = div_rc_w((float)((double)vv * (double)a.s_qk), a.rdiv);
           // -inf for padded columns: an add of a selected constant, so no branch
-          const float y = div_rc_w(d, a.rdiv) + (n < T ? 0.0f : -__builtin_inff());
+          y = y + (n < T ? 0.0f : -__builtin_inff());
           e[c][r] = y;
           mx = y > mx ? y : mx;
         }
@@ -227,6 +244,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     }
     const float tot = n2 ? leaf[0] + leaf[1] : leaf[0];
     const double rtot = 1.0 / (double)tot;
+    const float kpf = (float)(rtot * a.rs_p);  // t = e / tot / s_p within |t| 2^-22 of e * kpf
     // ---- P = quantize(e / tot): 4 packed bytes per (tile, group), row sums
     int dw[NT][4];
     int rp = 0;
@@ -235,11 +253,25 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         uint32_t packed = 0;
+        int qs[4];
+        if constexpr (FAST) {
+          bool sl[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) qs[j] = quant_filter(e[c][4 * qq + j] * kpf, a.zp_p_f, a.lo_f, a.hi_f, &sl[j]);
+          if (__builtin_expect(__any(sl[0] | sl[1] | sl[2] | sl[3]), 0)) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (sl[j]) qs[j] = quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            qs[j] = quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int n = c * 32 + 8 * qq + 4 * h + j;
-          const int qv = quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) &
-                         -(int)(n < T);  // padded columns: 0
+          const int qv = qs[j] & -(int)(n < T);  // padded columns: 0
           rp += qv;
           packed |= ((uint32_t)(qv & 0xff)) << (8 * j);
         }
@@ -278,13 +310,28 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         const int d0 = j * 32 + 8 * qq + 4 * h;
         const v4i cv = *reinterpret_cast<const v4i*>(colV + d0);
         uint32_t packed = 0;
+        int qs[4];
+        float o[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const int vv = acc2[j][4 * qq + jj] - rowp - cv[jj];
-          const float o = (float)((double)vv * (double)a.s_pv);
-          const int qv = quant_w(o, a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
-          packed |= ((uint32_t)(qv & 0xff)) << (8 * jj);
+          o[jj] = FAST ? (float)vv * a.s_pv : (float)((double)vv * (double)a.s_pv);
         }
+        if constexpr (FAST) {
+          bool sl[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) qs[jj] = quant_filter(o[jj] * a.rs_ctx_f, a.zp_ctx_f, a.lo_f, a.hi_f, &sl[jj]);
+          if (__builtin_expect(__any(sl[0] | sl[1] | sl[2] | sl[3]), 0)) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              if (sl[jj]) qs[jj] = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
+          }
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) qs[jj] = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) packed |= ((uint32_t)(qs[jj] & 0xff)) << (8 * jj);
         if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -346,12 +393,30 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   a.zp_ctx = (double)p->zp_ctx;
   a.lo = -__builtin_ldexp(1.0, p->bit_width - 1);
   a.hi = __builtin_ldexp(1.0, p->bit_width - 1) - 1.0;
+  a.inv_div = 1.0f / p->div;
+  a.rs_ctx_f = (float)a.rs_ctx;
+  a.zp_p_f = (float)p->zp_p;
+  a.zp_ctx_f = (float)p->zp_ctx;
+  a.lo_f = (float)a.lo;
+  a.hi_f = (float)a.hi;
+  // FAST: |acc - zero-point term| < 2^24 for the scores and the context (f32 dequant is
+  // then the f64 one), the Div is an exact power of two, |zp_ctx| small
+  const double qm = __builtin_ldexp(1.0, p->bit_width - 1);
+  const double bs = 64.0 * (qm * qm + qm * (double)(llabs(p->zq) + llabs(p->zk)) + (double)llabs(p->zq * p->zk));
+  const double bp = (double)T * (qm * qm + qm * (double)(llabs(p->zp_p) + llabs(p->zv)) + (double)llabs(p->zp_p * p->zv));
+  int dexp = 0;
+  const float dm = frexpf(p->div, &dexp);
+  const bool fast = bs < 16777216.0 && bp < 16777216.0 && dm == 0.5f && llabs(p->zp_ctx) < (1 << 20) &&
+                    !getenv("NQK_ATTN_EXACT");
   const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + (size_t)(NT * 32 + 64) * 4;
   const dim3 grid((unsigned)batch_heads);
-  switch (T == 197 ? 0 : NT) {
-#define A(n) case n: hipLaunchKernelGGL((k_attention<n, 0>), grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;
-    case 0:  // ViT at 224 px (196 patches + CLS): the pairwise plan and pads fold at compile time
-      hipLaunchKernelGGL((k_attention<7, 197>), grid, dim3(256), shm, stream(), q, k, v, ctx, a);
+  switch (T == 197 ? (fast ? -1 : 0) : NT) {
+#define A(n) case n: hipLaunchKernelGGL((k_attention<n, 0, false>), grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;
+    case -1:  // ViT at 224 px (196 patches + CLS): the pairwise plan and pads fold at compile time
+      hipLaunchKernelGGL((k_attention<7, 197, true>), grid, dim3(256), shm, stream(), q, k, v, ctx, a);
+      break;
+    case 0:
+      hipLaunchKernelGGL((k_attention<7, 197, false>), grid, dim3(256), shm, stream(), q, k, v, ctx, a);
       break;
     A(1) A(2) A(3) A(4) A(5) A(6) A(7)
 #undef A
