@@ -674,54 +674,69 @@ k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float
 }
 
 // LayerNorm + quantize with the whole NumPy pairwise tree in registers, for rows whose
-// plan is a complete binary tree of NL equal leaves of LF (multiple of 8) columns
-// (768 = 8 x 96 for ViT-Base): lane (leaf, j) owns columns leaf*LF + j + 8i, i.e.
-// exactly NumPy's accumulator r[j] of that leaf, summed in increasing i; the
+// plan is a complete binary tree of NL equal leaves of 96 columns (768 = 8 x 96 for
+// ViT-Base): lane (leaf, g) owns NumPy's accumulators r[4g..4g+3] of that leaf, i.e.
+// columns leaf*96 + 8i + 4g + (0..3) — one float4 per i, summed in increasing i; the
 // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) combine and the leaf tree are xor-butterflies
-// (float addition is commutative, only the grouping matters).  One row per NL*8 lanes.
-template <int NL, int LF>
+// (float addition is commutative, only the grouping matters).  2*NL lanes per row,
+// 64 / (2*NL) rows per wave; every load and store is 16 / 4 bytes per lane.
+template <int NL>
 __global__ void __launch_bounds__(256)
 k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
                int8_t* __restrict__ out, int64_t rows, float eps, float s, double rs, double zp, double lo,
                double hi) {
-  constexpr int LPR = NL * 8, NI = LF / 8, COLS = NL * LF;
+  constexpr int LF = 96, LPR = NL * 2, NI = LF / 8, COLS = NL * LF;
   const int lane = threadIdx.x & 63;
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
-  const int u = lane % LPR, leaf = u >> 3, j = u & 7;
+  const int u = lane % LPR, leaf = u >> 1, grp = u & 1;
   const bool ok = row < rows;
-  const float* xr = x + (ok ? row : 0) * COLS + leaf * LF + j;
-  float xv[NI];
+  const int c0 = leaf * LF + 4 * grp;
+  const float* xr = x + (ok ? row : 0) * COLS + c0;
+  float4 xv[NI];
 #pragma unroll
-  for (int i = 0; i < NI; ++i) xv[i] = xr[8 * i];
-  float acc = xv[0];
+  for (int i = 0; i < NI; ++i) xv[i] = *reinterpret_cast<const float4*>(xr + 8 * i);
+  float a0 = xv[0].x, a1 = xv[0].y, a2 = xv[0].z, a3 = xv[0].w;
 #pragma unroll
-  for (int i = 1; i < NI; ++i) acc = acc + xv[i];
+  for (int i = 1; i < NI; ++i) {
+    a0 = a0 + xv[i].x; a1 = a1 + xv[i].y; a2 = a2 + xv[i].z; a3 = a3 + xv[i].w;
+  }
+  float acc = (a0 + a1) + (a2 + a3);
 #pragma unroll
   for (int m = 1; m < LPR; m <<= 1) acc = acc + __shfl_xor(acc, m, 64);
   const float fcols = (float)COLS;
-  const float mean = acc / fcols;
-  const float nmean = -mean;
-  float dv[NI];
+  const float nmean = -(acc / fcols);
 #pragma unroll
-  for (int i = 0; i < NI; ++i) dv[i] = xv[i] + nmean;
-  float v2 = dv[0] * dv[0];
+  for (int i = 0; i < NI; ++i) {
+    xv[i].x = xv[i].x + nmean; xv[i].y = xv[i].y + nmean; xv[i].z = xv[i].z + nmean; xv[i].w = xv[i].w + nmean;
+  }
+  a0 = xv[0].x * xv[0].x; a1 = xv[0].y * xv[0].y; a2 = xv[0].z * xv[0].z; a3 = xv[0].w * xv[0].w;
 #pragma unroll
-  for (int i = 1; i < NI; ++i) v2 = v2 + dv[i] * dv[i];
+  for (int i = 1; i < NI; ++i) {
+    a0 = a0 + xv[i].x * xv[i].x; a1 = a1 + xv[i].y * xv[i].y;
+    a2 = a2 + xv[i].z * xv[i].z; a3 = a3 + xv[i].w * xv[i].w;
+  }
+  float v2 = (a0 + a1) + (a2 + a3);
 #pragma unroll
   for (int m = 1; m < LPR; m <<= 1) v2 = v2 + __shfl_xor(v2, m, 64);
   const float var = v2 / fcols;
   const float inv = 1.0f / __builtin_sqrtf(var + eps);
   if (!ok) return;
-  int8_t* orow = out + row * COLS + leaf * LF + j;
-  const float* gg = g + leaf * LF + j;
-  const float* bb = b + leaf * LF + j;
+  int8_t* orow = out + row * COLS + c0;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const float y = ((dv[i] * inv) * gg[8 * i]) + bb[8 * i];
-    const float t = (float)((double)y * rs);
-    const double uu = zp + (double)t;
-    const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
-    orow[8 * i] = (int8_t)q;
+    const float4 gg = *reinterpret_cast<const float4*>(g + c0 + 8 * i);
+    const float4 bb = *reinterpret_cast<const float4*>(b + c0 + 8 * i);
+    const float y[4] = {((xv[i].x * inv) * gg.x) + bb.x, ((xv[i].y * inv) * gg.y) + bb.y,
+                        ((xv[i].z * inv) * gg.z) + bb.z, ((xv[i].w * inv) * gg.w) + bb.w};
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float t = (float)((double)y[k] * rs);
+      const double uu = zp + (double)t;
+      const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
+      packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(orow + 8 * i) = packed;
   }
 }
 
@@ -943,16 +958,17 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
   bool eq = p.balanced && p.nleaf >= 1;
   for (int l = 0; eq && l < p.nleaf; ++l) eq = p.len[l] == 96;
   const bool snormal = __builtin_fabsf(scale) >= 0x1p-100f && __builtin_fabsf(scale) <= 0x1p100f;
-  if (eq && snormal && (p.nleaf == 8 || p.nleaf == 4 || p.nleaf == 2)) {
+  const bool al = ((((uintptr_t)x) | ((uintptr_t)gamma) | ((uintptr_t)beta)) & 15) == 0 && (((uintptr_t)out) & 3) == 0;
+  if (eq && snormal && al && (p.nleaf == 8 || p.nleaf == 4 || p.nleaf == 2)) {
     const double rs = 1.0 / (double)scale;
-    const int64_t lanes = rows * p.nleaf * 8;
+    const int64_t lanes = rows * p.nleaf * 2;
     const unsigned grid = (unsigned)((lanes + 255) / 256);
     switch (p.nleaf) {
-      case 8: hipLaunchKernelGGL((k_ln_quant_reg<8, 96>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
+      case 8: hipLaunchKernelGGL((k_ln_quant_reg<8>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
                                  eps, scale, rs, (double)zp, lo, hi); break;
-      case 4: hipLaunchKernelGGL((k_ln_quant_reg<4, 96>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
+      case 4: hipLaunchKernelGGL((k_ln_quant_reg<4>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
                                  eps, scale, rs, (double)zp, lo, hi); break;
-      default: hipLaunchKernelGGL((k_ln_quant_reg<2, 96>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out,
+      default: hipLaunchKernelGGL((k_ln_quant_reg<2>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out,
                                   rows, eps, scale, rs, (double)zp, lo, hi); break;
     }
     return launch_status("nqk_ln_quant(reg)");
