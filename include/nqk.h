@@ -135,6 +135,14 @@ int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch, int64_t M
 
 /* im2col for Conv (numpy_helper.py:18-70): x NCHW f32 -> cols[N*Ho*Wo][KH*KW*C]
  * (column order kh, kw, c), zero padding pads = (ph0, pw0, ph1, pw1). */
+/* ViT patch embedding in one GEMM (plan.py FusedEmbed): Conv as im2col . W in the BLAS
+ * order (nqk_sgemm), + bias, NCHW -> [B, HW, N] Reshape/Transpose, Concat behind the class
+ * token, + position embedding (model.py Conv/Reshape/Transpose/Concat/Add, in the node
+ * loop's rounding order):  out[b][0][n] = cls[n] + pos[0][n],
+ *   out[b][1+t][n] = (sgemm(cols, w)[b*hw + t][n] + bias[n]) + pos[1+t][n].
+ * cols [images*hw][K] (nqk_im2col), w [K][N], pos [hw+1][N], out [images][hw+1][N]; K even. */
+int nqk_sgemm_embed(const float* cols, const float* w, const float* bias, const float* cls, const float* pos,
+                    float* out, int64_t images, int64_t hw, int64_t N, int64_t K);
 int nqk_im2col(const float* x, float* cols, int64_t n, int64_t c, int64_t h, int64_t w,
                int64_t kh, int64_t kw, int64_t ph0, int64_t pw0, int64_t sh, int64_t sw,
                int64_t ho, int64_t wo);

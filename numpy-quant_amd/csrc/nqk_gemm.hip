@@ -224,10 +224,21 @@ k_sgemm_blas(const float* __restrict__ A, const float* __restrict__ B, float* __
 // bits at the MFMA rate.  128x128 tile, 4 waves (2x2, 64x64 each = 2x2 tiles of 32x32),
 // k-tiles of 16 staged k-major in LDS (one f32 per lane per MFMA operand).  Needs every
 // K-block end even (K even), since one MFMA consumes k and k+1.
+// EMBED epilogue (ViT patch embedding, plan.py FusedEmbed): row m = image * HW + patch of
+// the im2col GEMM goes to out[image][1 + patch][n] = (C + bias[n]) + pos[1 + patch][n],
+// i.e. Conv's bias add, the NCHW -> [B, HW, C] Reshape/Transpose, the Concat behind the
+// class token and the position-embedding Add, in the node loop's order of roundings.
+struct EmbedEpi {
+  const float* bias;
+  const float* pos;  // [HW + 1][N]
+  int64_t hw;
+};
+
+template <bool EMBED>
 __global__ void __launch_bounds__(256)
 k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
              int64_t N, int64_t K, int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc,
-             BatchMap bm, int64_t a_ms, int64_t b_ms, int64_t c_ms, KBlocks kb) {
+             BatchMap bm, int64_t a_ms, int64_t b_ms, int64_t c_ms, KBlocks kb, EmbedEpi ee) {
   typedef float v16f __attribute__((ext_vector_type(16)));
   __shared__ float sa[2][16][128 + 4], sb[2][16][128 + 4];
   const int64_t bz = blockIdx.z;
@@ -311,9 +322,27 @@ k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (gm < M && gn < N) C[gm * ldc + gn] = tot[i][j][r];
+        if (gm < M && gn < N) {
+          if constexpr (EMBED) {
+            const int64_t img = gm / ee.hw, t = gm - img * ee.hw;
+            const float y = tot[i][j][r] + ee.bias[gn];
+            C[(img * (ee.hw + 1) + 1 + t) * N + gn] = y + ee.pos[(1 + t) * N + gn];
+          } else {
+            C[gm * ldc + gn] = tot[i][j][r];
+          }
+        }
       }
     }
+}
+
+// class-token rows of the EMBED output: out[image][0][n] = cls[n] + pos[0][n]
+__global__ void k_embed_cls(const float* __restrict__ cls, const float* __restrict__ pos, float* __restrict__ out,
+                            int64_t images, int64_t hw, int64_t n) {
+  const int64_t total = images * n, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t img = i / n, c = i - img * n;
+    out[img * (hw + 1) * n + c] = cls[c] + pos[c];
+  }
 }
 
 __global__ void k_im2col(const float* __restrict__ x, float* __restrict__ cols, int64_t n, int64_t c, int64_t h,
@@ -399,14 +428,31 @@ extern "C" int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch
   if ((K & 1) == 0 && K > 0 && M * N >= 128 * 128 && !getenv("NQK_SGEMM_VALU")) {
     dim3 g2((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128), (unsigned)batch);
     if ((M + 127) / 128 > 65535) return fail("nqk_sgemm: grid too large");
-    hipLaunchKernelGGL(k_sgemm_mfma, g2, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk, b_sk, b_sn, ldc, m,
-                       a_mat_stride, b_mat_stride, c_mat_stride, kb);
+    hipLaunchKernelGGL(k_sgemm_mfma<false>, g2, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk, b_sk, b_sn, ldc,
+                       m, a_mat_stride, b_mat_stride, c_mat_stride, kb, EmbedEpi{nullptr, nullptr, 1});
     return launch_status("nqk_sgemm(mfma)");
   }
   dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64), (unsigned)batch);
   hipLaunchKernelGGL(k_sgemm_blas, grid, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk, b_sk, b_sn, ldc, m,
                      a_mat_stride, b_mat_stride, c_mat_stride, kb);
   return launch_status("nqk_sgemm");
+}
+
+extern "C" int nqk_sgemm_embed(const float* cols, const float* w, const float* bias, const float* cls,
+                               const float* pos, float* out, int64_t images, int64_t hw, int64_t N, int64_t K) {
+  const int64_t M = images * hw;
+  if (M <= 0 || N <= 0) return 0;
+  if ((K & 1) || K <= 0) return fail("nqk_sgemm_embed: K must be even (MFMA k pairs)");
+  if ((M + 127) / 128 > 65535) return fail("nqk_sgemm_embed: grid too large");
+  KBlocks kb;
+  if (blas_kblocks(K, &kb)) return fail("nqk_sgemm_embed: K too large for the BLAS blocking table");
+  const BatchMap m = batch_map(nullptr);
+  dim3 g2((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128), 1);
+  hipLaunchKernelGGL(k_sgemm_mfma<true>, g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1, N,
+                     (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
+  if (int rc = launch_status("nqk_sgemm_embed")) return rc;
+  hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);
+  return launch_status("nqk_sgemm_embed(cls)");
 }
 
 extern "C" int nqk_im2col(const float* x, float* cols, int64_t n, int64_t c, int64_t h, int64_t w, int64_t kh,

@@ -29,8 +29,10 @@ EPI_QKV, EPI_SCORES, EPI_PV, EPI_RESID, EPI_GELU = 0, 1, 2, 3, 4
 
 _EPI_NAMES = {EPI_QKV: "qkv", EPI_SCORES: "scores", EPI_PV: "pv", EPI_RESID: "resid", EPI_GELU: "gelu"}
 
-# module switch: the one-kernel attention (nqk_attention_fused) where it applies
+# module switches: the one-kernel attention (nqk_attention_fused) and the one-GEMM
+# patch embedding (nqk_sgemm_embed) where they apply
 FUSED_ATTENTION = True
+FUSED_EMBED = True
 
 
 Epilogue = _lib.Epilogue
@@ -243,6 +245,139 @@ class LayerMatch:
         self.tokens, self.heads, self.hdim = int(shp[1]), int(shp[2]), int(shp[3])
 
 
+# ----------------------------------------------------------------------------- patch embedding
+def _const_ints(value):
+    arr, _ = _const_node_value(value)
+    return np.asarray(arr).reshape(-1).astype(np.int64)
+
+
+class EmbedMatch:
+    """ViT patch embedding (models/vit graphs):
+        Conv(x, W, b)  -> Reshape(., Concat(Slice(Shape(.), [0], [2], [0]), [-1]))
+        -> Transpose([0, 2, 1]) -> Concat([Expand(cls, .), .], axis=1) -> Add(., pos)
+    computed by one im2col GEMM with a fused epilogue (nqk_sgemm_embed).  The Conv
+    output is never materialised: its Shape consumer sees a shape-only placeholder."""
+
+    def __init__(self, qmodel, conv):
+        self.nodes = set()
+        take = self.nodes.add
+        if conv.op != "Conv" or len(conv.inputs) != 3:
+            raise NoMatch("Conv with bias expected")
+        x, w, b = conv.inputs
+        if _is_const(x) or not (_is_const(w) and _is_const(b)):
+            raise NoMatch("Conv(x, const W, const b) expected")
+        a = conv.attrs
+        kh, kw = (int(v) for v in a.get("kernel_shape", w.data.dev.shape[2:]))
+        if list(a.get("strides", [1, 1])) != [kh, kw] or any(int(p) for p in a.get("pads", [0, 0, 0, 0])):
+            raise NoMatch("patchify Conv (stride = kernel, no padding) expected")
+        if any(int(d) != 1 for d in a.get("dilations", [1, 1])) or int(a.get("group", 1)) != 1:
+            raise NoMatch("plain Conv expected")
+        take(conv)
+        self.conv, self.x, self.w, self.b = conv, x, w, b
+        self.kh, self.kw = kh, kw
+        cout = conv.outputs[0]
+        users = cout.outputs
+        rs = [u for u in users if u.op == "Reshape"]
+        shp = [u for u in users if u.op == "Shape"]
+        if len(rs) != 1 or len(rs) + len(shp) != len(users):
+            raise NoMatch("Conv output must feed one Reshape (+ Shape)")
+        rs = rs[0]
+        take(rs)
+        # reshape target = Concat(Slice(Shape(conv), [0], [2], [0]), [-1])  ->  [B, C, H*W]
+        cat = rs.inputs[1].inputs[0] if rs.inputs[1].inputs else None
+        if cat is None or cat.op != "Concat" or len(cat.inputs) != 2:
+            raise NoMatch("reshape target")
+        sl = cat.inputs[0].inputs[0] if cat.inputs[0].inputs else None
+        if sl is None or sl.op != "Slice" or sl.inputs[0].inputs[0].op != "Shape" or \
+                sl.inputs[0].inputs[0].inputs[0] is not cout:
+            raise NoMatch("reshape target slice")
+        if list(_const_ints(sl.inputs[1])) != [0] or list(_const_ints(sl.inputs[2])) != [2] or \
+                list(_const_ints(sl.inputs[3])) != [0] or list(_const_ints(cat.inputs[1])) != [-1]:
+            raise NoMatch("reshape target values")
+        tr = _consumer(rs.outputs[0], "Transpose")
+        if list(tr.attrs["perm"]) != [0, 2, 1]:
+            raise NoMatch("patch transpose")
+        take(tr)
+        cc = _consumer(tr.outputs[0], "Concat")
+        if cc.attrs.get("axis") != 1 or len(cc.inputs) != 2 or cc.inputs[1] is not tr.outputs[0]:
+            raise NoMatch("class-token concat")
+        take(cc)
+        ex = cc.inputs[0].inputs[0] if cc.inputs[0].inputs else None
+        if ex is None or ex.op != "Expand" or not _is_const(ex.inputs[0]) or len(cc.inputs[0].outputs) != 1:
+            raise NoMatch("class-token expand")
+        take(ex)
+        self.expand, self.cls = ex, ex.inputs[0]
+        add = _consumer(cc.outputs[0], "Add")
+        others = [i for i in add.inputs if i is not cc.outputs[0]]
+        if len(others) != 1 or not _is_const(others[0]) or add.inputs[0] is not cc.outputs[0]:
+            raise NoMatch("position-embedding add")
+        take(add)
+        self.pos, self.add, self.conv_out = others[0], add, cout
+        for node in self.nodes:
+            for o in node.outputs:
+                if o is add.outputs[0] or o is cout:
+                    continue
+                for u in o.outputs:
+                    if u not in self.nodes:
+                        raise NoMatch(f"{o.name} escapes the embedding")
+
+
+class _ShapeOnly:
+    """Stand-in value for a tensor that is never materialised: only its shape is read
+    (ONNX Shape node, model.py Shape -> x.shape)."""
+
+    def __init__(self, shape):
+        self._shape = tuple(int(s) for s in shape)
+
+    @property
+    def shape(self):
+        from .tensor import ITensor
+        return ITensor(np.array(self._shape, dtype=np.int64))
+
+
+class FusedEmbed:
+    def __init__(self, qmodel, m: EmbedMatch):
+        self.m = m
+        deq = qmodel._dequant_input
+        W = deq(m.w).dev
+        self.kout, cin = W.shape[0], W.shape[1]
+        self.kk = m.kh * m.kw * cin
+        from .device import permute
+        # weight matrix [(kh, kw, c), kout] as fconv2d builds it (tensor.py)
+        self.wm = permute(W, [2, 3, 1, 0]).reshape((self.kk, self.kout))
+        self.bias = deq(m.b).dev
+        self.cls = deq(m.cls).dev
+        self.posv = deq(m.pos).dev
+        if self.kk % 2 or self.bias.size != self.kout or self.cls.size != self.kout:
+            raise NoMatch("embedding dimensions")
+
+    def pre(self, qmodel):
+        """at the Conv's position: the shape-only placeholder for the Shape consumer"""
+        m = self.m
+        n, c, h, w = m.x.data.dev.shape
+        m.conv_out.data = _ShapeOnly((n, self.kout, h // m.kh, w // m.kw))
+
+    def run(self, qmodel):
+        m = self.m
+        x = qmodel._dequant_input(m.x) if isinstance(m.x.data, QTensor) else m.x.data
+        n, c, h, w = x.dev.shape
+        cols, ho, wo = KM.im2col(x.dev, m.kh, m.kw, (0, 0, 0, 0), (m.kh, m.kw))
+        hw = ho * wo
+        if self.posv.size != (hw + 1) * self.kout:
+            raise ValueError("position embedding does not match the patch grid")
+        eshape = np.asarray(m.expand.inputs[1].data.data).reshape(-1)
+        if eshape.size != 3 or int(eshape[0]) != n:
+            raise ValueError(f"class-token Expand shape {eshape} does not match the batch {n}")
+        out = DeviceArray((n, hw + 1, self.kout), np.float32)
+        t0 = KM.TIMER.begin() if KM.TIMER is not None else None
+        _lib.call("nqk_sgemm_embed", cols.vp, self.wm.vp, self.bias.vp, self.cls.vp, self.posv.vp, out.vp,
+                  n, hw, self.kout, self.kk)
+        if t0 is not None:
+            KM.TIMER.end("embed_sgemm", t0, (0, 4 * (n * hw * self.kk + self.kk * self.kout + n * (hw + 1) * self.kout)))
+        m.add.outputs[0].data = FTensor(out)
+        m.conv_out.data = None
+
+
 # ----------------------------------------------------------------------------- fused layer
 class FusedLayer:
     def __init__(self, qmodel, m: LayerMatch):
@@ -448,6 +583,18 @@ class Plan:
         self.ws = Workspace()
         self.fused = 0
         claimed = {}
+        self.embeds = 0
+        for node in qmodel.nodes:
+            if node.op != "Conv" or not FUSED_EMBED:
+                continue
+            try:
+                em = EmbedMatch(qmodel, node)
+                fe = FusedEmbed(qmodel, em)
+            except NoMatch:
+                continue
+            for n in em.nodes:
+                claimed[n] = fe
+            self.embeds += 1
         if qmodel.bit_width <= 8 and qmodel.bit_width >= 2:
             for node in qmodel.nodes:
                 if node.op != "LayerNormalization" or node in claimed:
@@ -457,6 +604,8 @@ class Plan:
                     layer = FusedLayer(qmodel, m)
                 except NoMatch:
                     continue
+                if any(n in claimed for n in m.nodes):
+                    continue
                 for n in m.nodes:
                     claimed[n] = layer
         placed = set()
@@ -464,6 +613,11 @@ class Plan:
             layer = claimed.get(node)
             if layer is None:
                 self.steps.append(("node", node))
+            elif isinstance(layer, FusedEmbed):
+                if node is layer.m.conv:
+                    self.steps.append(("embed_pre", layer))
+                elif node is layer.m.add:
+                    self.steps.append(("embed", layer))
             elif id(layer) not in placed:
                 placed.add(id(layer))
                 self.steps.append(("layer", layer))
@@ -473,6 +627,10 @@ class Plan:
         for kind, obj in self.steps:
             if kind == "node":
                 qmodel._run_node(obj, times, profile)
+            elif kind == "embed_pre":
+                obj.pre(qmodel)
+            elif kind == "embed":
+                obj.run(qmodel)
             else:
                 obj.run(self.ws)
 
