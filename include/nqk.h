@@ -143,6 +143,11 @@ int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch, int64_t M
  * cols [images*hw][K] (nqk_im2col), w [K][N], pos [hw+1][N], out [images][hw+1][N]; K even. */
 int nqk_sgemm_embed(const float* cols, const float* w, const float* bias, const float* cls, const float* pos,
                     float* out, int64_t images, int64_t hw, int64_t N, int64_t K);
+/* im2col of a patchify Conv (stride = kernel, no padding, numpy_helper.py:18-70) fused with
+ * the dequantize of its int8 input (numpy_quantization.py:37-41):
+ * cols[(b,oy,ox)][(ki,kj,ci)] = f32((q[b][ci][oy*kh+ki][ox*kw+kj] - zp) * scale). */
+int nqk_patchify_dequant(const int8_t* q, float* cols, int64_t n, int64_t c, int64_t h, int64_t w, int64_t kh,
+                         int64_t kw, float scale, int64_t zp);
 int nqk_im2col(const float* x, float* cols, int64_t n, int64_t c, int64_t h, int64_t w,
                int64_t kh, int64_t kw, int64_t ph0, int64_t pw0, int64_t sh, int64_t sw,
                int64_t ho, int64_t wo);

@@ -235,7 +235,7 @@ struct EmbedEpi {
 };
 
 template <bool EMBED>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 2)
 k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
              int64_t N, int64_t K, int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc,
              BatchMap bm, int64_t a_ms, int64_t b_ms, int64_t c_ms, KBlocks kb, EmbedEpi ee) {
@@ -324,9 +324,9 @@ k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __
         const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (gm < M && gn < N) {
           if constexpr (EMBED) {
-            const int64_t img = gm / ee.hw, t = gm - img * ee.hw;
+            const uint32_t img = (uint32_t)gm / (uint32_t)ee.hw, t = (uint32_t)gm - img * (uint32_t)ee.hw;
             const float y = tot[i][j][r] + ee.bias[gn];
-            C[(img * (ee.hw + 1) + 1 + t) * N + gn] = y + ee.pos[(1 + t) * N + gn];
+            C[((int64_t)img * (ee.hw + 1) + 1 + t) * N + gn] = y + ee.pos[(1 + (int64_t)t) * N + gn];
           } else {
             C[gm * ldc + gn] = tot[i][j][r];
           }
@@ -342,6 +342,37 @@ __global__ void k_embed_cls(const float* __restrict__ cls, const float* __restri
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     const int64_t img = i / n, c = i - img * n;
     out[img * (hw + 1) * n + c] = cls[c] + pos[c];
+  }
+}
+
+// im2col of a patchify Conv (stride = kernel, no padding) fused with the dequantize of
+// its quantized input (model.py: QModel dequantizes a QTensor before a float op):
+// cols[(b, oy, ox)][(ki, kj, ci)] = f32((q[b][ci][oy*kh + ki][ox*kw + kj] - zp) * s).
+// f32 (q - zp) * s is the f64 dequant exactly: |q - zp| < 2^24, one rounding.
+// One thread per (patch row m, ki): kw * c consecutive outputs.
+template <bool VEC16>
+__global__ void k_patchify_dequant(const int8_t* __restrict__ q, float* __restrict__ cols, int64_t n, int64_t c,
+                                   int64_t h, int64_t w, int64_t kh, int64_t kw, float s, float zpf) {
+  const int64_t ho = h / kh, wo = w / kw, M = n * ho * wo;
+  const int64_t total = M * kh, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t m = i / kh, ki = i - m * kh;
+    const int64_t b = m / (ho * wo), p = m - b * (ho * wo), oy = p / wo, ox = p - oy * wo;
+    float* dst = cols + m * (kh * kw * c) + ki * kw * c;
+    for (int64_t ci = 0; ci < c; ++ci) {
+      const int8_t* src = q + ((b * c + ci) * h + oy * kh + ki) * w + ox * kw;
+      if constexpr (VEC16) {
+        const int4 v = *reinterpret_cast<const int4*>(src);
+        const int wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int kj = 0; kj < 16; ++kj) {
+          const int qv = (int)(int8_t)(wv[kj >> 2] >> (8 * (kj & 3)));
+          dst[kj * c + ci] = ((float)qv - zpf) * s;
+        }
+      } else {
+        for (int64_t kj = 0; kj < kw; ++kj) dst[kj * c + ci] = ((float)src[kj] - zpf) * s;
+      }
+    }
   }
 }
 
@@ -453,6 +484,22 @@ extern "C" int nqk_sgemm_embed(const float* cols, const float* w, const float* b
   if (int rc = launch_status("nqk_sgemm_embed")) return rc;
   hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);
   return launch_status("nqk_sgemm_embed(cls)");
+}
+
+extern "C" int nqk_patchify_dequant(const int8_t* q, float* cols, int64_t n, int64_t c, int64_t h, int64_t w,
+                                    int64_t kh, int64_t kw, float scale, int64_t zp) {
+  if (kh <= 0 || kw <= 0 || h % kh || w % kw) return fail("nqk_patchify_dequant: the kernel must tile the image");
+  if (zp < -(1 << 20) || zp > (1 << 20)) return fail("nqk_patchify_dequant: zero point out of range");
+  const int64_t total = n * (h / kh) * (w / kw) * kh;
+  if (total <= 0) return 0;
+  const bool vec = kw == 16 && (w % 16) == 0 && (((uintptr_t)q) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(k_patchify_dequant<true>, dim3(grid_for(total)), dim3(kThreads), 0, stream(), q, cols, n, c, h,
+                       w, kh, kw, scale, (float)zp);
+  else
+    hipLaunchKernelGGL(k_patchify_dequant<false>, dim3(grid_for(total)), dim3(kThreads), 0, stream(), q, cols, n, c,
+                       h, w, kh, kw, scale, (float)zp);
+  return launch_status("nqk_patchify_dequant");
 }
 
 extern "C" int nqk_im2col(const float* x, float* cols, int64_t n, int64_t c, int64_t h, int64_t w, int64_t kh,

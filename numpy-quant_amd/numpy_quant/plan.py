@@ -359,10 +359,20 @@ class FusedEmbed:
 
     def run(self, qmodel):
         m = self.m
-        x = qmodel._dequant_input(m.x) if isinstance(m.x.data, QTensor) else m.x.data
-        n, c, h, w = x.dev.shape
-        cols, ho, wo = KM.im2col(x.dev, m.kh, m.kw, (0, 0, 0, 0), (m.kh, m.kw))
+        xd = m.x.data
+        n, c, h, w = xd.dev.shape
+        ho, wo = h // m.kh, w // m.kw
         hw = ho * wo
+        zp = xd.zero_point
+        if isinstance(xd, QTensor) and xd._bias is None and xd.dev.dtype == np.int8 and h % m.kh == 0 and w % m.kw == 0 and \
+                (zp is None or np.ndim(zp) == 0):
+            # dequantize fused into the patch gather (the QTensor is read once, as int8)
+            cols = DeviceArray((n * hw, self.kk), np.float32)
+            _lib.call("nqk_patchify_dequant", xd.dev.vp, cols.vp, n, c, h, w, m.kh, m.kw,
+                      float(np.float32(xd.scale)), int(zp) if zp is not None else 0)
+        else:
+            x = qmodel._dequant_input(m.x) if isinstance(xd, QTensor) else xd
+            cols, ho, wo = KM.im2col(x.dev, m.kh, m.kw, (0, 0, 0, 0), (m.kh, m.kw))
         if self.posv.size != (hw + 1) * self.kout:
             raise ValueError("position embedding does not match the patch grid")
         eshape = np.asarray(m.expand.inputs[1].data.data).reshape(-1)

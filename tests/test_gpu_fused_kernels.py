@@ -69,3 +69,21 @@ def test_gelu_epilogue_filter_matches_exact_chain(s_out, zp, bw, monkeypatch):
         _gemm(EPI_GELU, a, bt, 1, M, N, K, K, K, None, 0, 0, e)
         outs.append(out.to_host())
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("n,c,h,w,kh,kw,zp", [(2, 3, 224, 224, 16, 16, -5), (1, 3, 32, 48, 16, 16, 0),
+                                             (3, 2, 12, 15, 4, 5, 7), (1, 1, 8, 8, 2, 2, -128)])
+def test_patchify_dequant_equals_dequantize_then_im2col(n, c, h, w, kh, kw, zp):
+    """Conv input path of the fused patch embedding: dequantize (numpy_quantization.py:37-41)
+    then numpy_helper.py:18-70 sliding windows, in one pass over the int8 input."""
+    from numpy_quant import _lib
+    from numpy_quant import kernels as KM
+    from numpy_quant.device import DeviceArray
+    rng = np.random.default_rng(h * w + c)
+    q = rng.integers(-128, 128, size=(n, c, h, w), dtype=np.int8)
+    s = np.float32(0.0173)
+    x = O.dequantize(q.astype(np.int64), s, np.int64(zp) if zp else None)
+    ref_cols, _, _ = KM.im2col(DeviceArray.from_host(x), kh, kw, (0, 0, 0, 0), (kh, kw))
+    cols = DeviceArray(ref_cols.shape, np.float32)
+    _lib.call("nqk_patchify_dequant", DeviceArray.from_host(q).vp, cols.vp, n, c, h, w, kh, kw, float(s), zp)
+    np.testing.assert_array_equal(cols.to_host(), ref_cols.to_host())
