@@ -33,6 +33,7 @@ _EPI_NAMES = {EPI_QKV: "qkv", EPI_SCORES: "scores", EPI_PV: "pv", EPI_RESID: "re
 # patch embedding (nqk_sgemm_embed) where they apply
 FUSED_ATTENTION = True
 FUSED_EMBED = True
+LN_GATHER = True
 
 
 Epilogue = _lib.Epilogue
@@ -388,6 +389,40 @@ class FusedEmbed:
         m.conv_out.data = None
 
 
+# ----------------------------------------------------------------------------- Gather after LN
+class LnGather:
+    """LayerNormalization (last axis) whose only consumer is a Gather along another axis
+    with constant indices (the ViT classifier reads the CLS token only): LayerNorm
+    normalises every row on its own, so Gather-then-LN equals LN-then-Gather bit for bit
+    and only the gathered rows are normalised.  The LN output is not materialised."""
+
+    def __init__(self, qmodel, ln):
+        if ln.op != "LayerNormalization":
+            raise NoMatch("LayerNormalization expected")
+        out = ln.outputs[0]
+        g = _only(out.outputs, "LN consumer")
+        if g.op != "Gather" or g.inputs[0] is not out:
+            raise NoMatch("Gather consumer expected")
+        idx = g.inputs[1]
+        if not (idx.inputs and idx.inputs[0].op == "Constant"):
+            raise NoMatch("constant Gather indices expected")
+        ax = int(ln.attrs.get("axis", -1))
+        gax = int(g.attrs.get("axis", 0))
+        if ax != -1 or gax in (-1,):
+            raise NoMatch("LN over the last axis, Gather over another one")
+        self.ln, self.g, self.nodes = ln, g, {ln, g}
+
+    def run(self, qmodel, times=None, profile=False):
+        from .model import onnx_operator_implementation
+        x = self.ln.inputs[0].data
+        if not isinstance(x, FTensor) or int(self.g.attrs.get("axis", 0)) % x.dev.ndim == x.dev.ndim - 1:
+            raise ValueError("LN/Gather pushdown needs a float input gathered off the last axis")
+        xs = x.take(self.g.inputs[1].data, axis=int(self.g.attrs.get("axis", 0)))
+        args = [xs] + [qmodel._dequant_input(v) if isinstance(v.data, QTensor) else v.data for v in self.ln.inputs[1:]]
+        self.g.outputs[0].data = onnx_operator_implementation("LayerNormalization", args, self.ln.attrs)[0]
+        self.ln.outputs[0].data = None
+
+
 # ----------------------------------------------------------------------------- fused layer
 class FusedLayer:
     def __init__(self, qmodel, m: LayerMatch):
@@ -605,6 +640,16 @@ class Plan:
             for n in em.nodes:
                 claimed[n] = fe
             self.embeds += 1
+        self.pushdowns = 0
+        for node in qmodel.nodes:
+            if node.op != "LayerNormalization" or not LN_GATHER:
+                continue
+            try:
+                lg = LnGather(qmodel, node)
+            except NoMatch:
+                continue
+            claimed[lg.ln] = claimed[lg.g] = lg
+            self.pushdowns += 1
         if qmodel.bit_width <= 8 and qmodel.bit_width >= 2:
             for node in qmodel.nodes:
                 if node.op != "LayerNormalization" or node in claimed:
@@ -623,6 +668,9 @@ class Plan:
             layer = claimed.get(node)
             if layer is None:
                 self.steps.append(("node", node))
+            elif isinstance(layer, LnGather):
+                if node is layer.g:
+                    self.steps.append(("ln_gather", layer))
             elif isinstance(layer, FusedEmbed):
                 if node is layer.m.conv:
                     self.steps.append(("embed_pre", layer))
@@ -641,6 +689,8 @@ class Plan:
                 obj.pre(qmodel)
             elif kind == "embed":
                 obj.run(qmodel)
+            elif kind == "ln_gather":
+                obj.run(qmodel, times, profile)
             else:
                 obj.run(self.ws)
 

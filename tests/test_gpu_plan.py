@@ -30,7 +30,7 @@ def test_plan_matches_reference_vit_b1():
     model = _vit(1, meta["seed"])
     qmodel = model.quantize_with(ref_qparams(meta["bw8"]["qparams"]), bit_width=8)
     plan = qmodel.compile()
-    assert plan.fused == 12 and plan.embeds == 1
+    assert plan.fused == 12 and plan.embeds == 1 and plan.pushdowns == 1
     out = qmodel([arrs["x_run"]])[0]
     np.testing.assert_array_equal(out, arrs["bw8_out"])
     # every layer output (residual stream) equals the reference's value
@@ -50,7 +50,7 @@ def test_plan_equals_eager(batch, bw):
     eager = qmodel([x])[0]
     layer_outs = {}
     plan = qmodel.compile()
-    assert plan.fused == 12 and plan.embeds == 1
+    assert plan.fused == 12 and plan.embeds == 1 and plan.pushdowns == 1
     for _, layer in [s for s in plan.steps if s[0] == "layer"]:
         layer_outs[layer.m.x_out.name] = None
     fused = qmodel([x])[0]
