@@ -359,17 +359,28 @@ __global__ void k_patchify_dequant(const int8_t* __restrict__ q, float* __restri
     const int64_t m = i / kh, ki = i - m * kh;
     const int64_t b = m / (ho * wo), p = m - b * (ho * wo), oy = p / wo, ox = p - oy * wo;
     float* dst = cols + m * (kh * kw * c) + ki * kw * c;
-    for (int64_t ci = 0; ci < c; ++ci) {
-      const int8_t* src = q + ((b * c + ci) * h + oy * kh + ki) * w + ox * kw;
-      if constexpr (VEC16) {
-        const int4 v = *reinterpret_cast<const int4*>(src);
-        const int wv[4] = {v.x, v.y, v.z, v.w};
+    if constexpr (VEC16) {
+      // c == 3 (RGB): the 48 outputs (kj, ci) are contiguous -> 12 float4 stores
+      int wv[3][4];
 #pragma unroll
-        for (int kj = 0; kj < 16; ++kj) {
-          const int qv = (int)(int8_t)(wv[kj >> 2] >> (8 * (kj & 3)));
-          dst[kj * c + ci] = ((float)qv - zpf) * s;
+      for (int ci = 0; ci < 3; ++ci) {
+        const int4 v = *reinterpret_cast<const int4*>(q + ((b * 3 + ci) * h + oy * kh + ki) * w + ox * 16);
+        wv[ci][0] = v.x; wv[ci][1] = v.y; wv[ci][2] = v.z; wv[ci][3] = v.w;
+      }
+#pragma unroll
+      for (int o = 0; o < 12; ++o) {
+        float f[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 4 * o + e, kj = j / 3, ci = j % 3;
+          const int qv = (int)(int8_t)(wv[ci][kj >> 2] >> (8 * (kj & 3)));
+          f[e] = ((float)qv - zpf) * s;
         }
-      } else {
+        *reinterpret_cast<float4*>(dst + 4 * o) = make_float4(f[0], f[1], f[2], f[3]);
+      }
+    } else {
+      for (int64_t ci = 0; ci < c; ++ci) {
+        const int8_t* src = q + ((b * c + ci) * h + oy * kh + ki) * w + ox * kw;
         for (int64_t kj = 0; kj < kw; ++kj) dst[kj * c + ci] = ((float)src[kj] - zpf) * s;
       }
     }
@@ -492,7 +503,7 @@ extern "C" int nqk_patchify_dequant(const int8_t* q, float* cols, int64_t n, int
   if (zp < -(1 << 20) || zp > (1 << 20)) return fail("nqk_patchify_dequant: zero point out of range");
   const int64_t total = n * (h / kh) * (w / kw) * kh;
   if (total <= 0) return 0;
-  const bool vec = kw == 16 && (w % 16) == 0 && (((uintptr_t)q) & 15) == 0;
+  const bool vec = kw == 16 && c == 3 && (w % 16) == 0 && (((uintptr_t)q) & 15) == 0 && (((uintptr_t)cols) & 15) == 0;
   if (vec)
     hipLaunchKernelGGL(k_patchify_dequant<true>, dim3(grid_for(total)), dim3(kThreads), 0, stream(), q, cols, n, c, h,
                        w, kh, kw, scale, (float)zp);
