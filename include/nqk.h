@@ -188,7 +188,9 @@ int nqk_where_f32(const int64_t* cond, const float* a, const float* b, float* ou
 enum nqk_epi { NQK_EPI_QKV = 0, NQK_EPI_SCORES = 1, NQK_EPI_PV = 2, NQK_EPI_RESID = 3, NQK_EPI_GELU = 4,
                NQK_EPI_NULL = 5 /* diagnostic: no stores (main-loop timing) */ };
 typedef struct nqk_epilogue {
-  int32_t zp_flags, bit_width, group_cols, tokens, heads, hdim, ld_out, pad0;
+  int32_t zp_flags, bit_width, group_cols, tokens, heads, hdim, ld_out;
+  int32_t col_absmax;                  /* max |col[n]| if known (0: unknown); lets the   */
+                                       /* epilogue dequantize in f32 when provably exact */
   int64_t zpa, zpb, kdim;              /* zero-point term: ROW / COL / KCONST flags; row  */
   const int64_t* row;                  /* sums of A and Bt are computed in-kernel unless  */
   const int64_t* col;                  /* `col` holds precomputed int64 column sums of B  */
@@ -239,7 +241,9 @@ int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_t* v, int8_
 
 /* Diagnostic: on the device, compares the fast-division variants of NumPy's exp and the
  * reference's erf (used by the fused kernels) with the IEEE-division ones on all 2^32
- * float inputs; adds the mismatch counts to counts_dev[0] (exp) / [1] (erf). */
+ * float inputs; adds the mismatch counts to counts_dev[0] (exp) / [1] (erf), and those of
+ * the attention kernel's non-positive-argument exp against NumPy's exp to [2] (all 2^31
+ * inputs x <= 0).  counts_dev and examples_dev hold 3 entries each. */
 int nqk_selftest_fastmath(unsigned long long* counts_dev, uint32_t* examples_dev);
 /* Diagnostic: checks the error bound of the GELU filter's cheap approximation on all
  * 2^32 inputs; stats_dev[0] = violations, [1] = an example, [2 + e] = max error per

@@ -198,7 +198,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     for (int c = 0; c < NT; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        e[c][r] = np_expf(e[c][r] + nm);  // -inf pads -> 0
+        e[c][r] = np_expf_nonpos(e[c][r] + nm);  // y - max <= 0; -inf pads -> 0
         if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
     // ---- NumPy pairwise sum: accumulators r[4h + j] of each leaf, in increasing n

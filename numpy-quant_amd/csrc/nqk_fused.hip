@@ -74,8 +74,9 @@ struct Epi {
   int tokens, heads, hdim, ld_out;
   double lo, hi;
   int gelu_filter;           // EPI_GELU: constants are the ViT GELU's (sqrt2, 1, 0.5)
-  float rsf, zpf, lof, hif;  // f32 RN(1/s_out), zp_out[0], lo, hi for the filter
-  float g_rel, g_abs;        // filter error terms, in units of t
+  float rsf[3], zpf[3];      // f32 RN(1/s_out), zp_out per group, for the rounding filters
+  float lof, hif;            // lo, hi as f32
+  float g_rel, g_abs;        // GELU filter error terms, in units of t
 };
 
 enum { EPI_QKV = 0, EPI_SCORES = 1, EPI_PV = 2, EPI_RESID = 3, EPI_GELU = 4, EPI_NULL = 5 };
@@ -157,6 +158,7 @@ struct EpiCol4 {
   float bias[4];
   float s_acc, s_out;  // per-lane copies of the column group's scalars (no dynamic
   double rs_out, zp;   // indexing into the kernel-argument struct inside the row loop)
+  float rsf, zpf;
   int8_t* out;
   int hh, dd;
 };
@@ -184,6 +186,8 @@ __device__ __forceinline__ EpiCol4 epi_col4(const Epi& e, int gn0, bool ok) {
   c.rs_out = g == 0 ? e.rs_out[0] : (g == 1 ? e.rs_out[1] : e.rs_out[2]);
   c.zp = g == 0 ? e.zp_out[0] : (g == 1 ? e.zp_out[1] : e.zp_out[2]);
   c.out = (int8_t*)(g == 0 ? e.out[0] : (g == 1 ? e.out[1] : e.out[2]));
+  c.rsf = g == 0 ? e.rsf[0] : (g == 1 ? e.rsf[1] : e.rsf[2]);
+  c.zpf = g == 0 ? e.zpf[0] : (g == 1 ? e.zpf[1] : e.zpf[2]);
   return c;
 }
 
@@ -214,12 +218,27 @@ __device__ __forceinline__ float dequant_elem(int32_t acc, int64_t colterm, floa
   return (float)(vd * (double)s_acc);
 }
 
-template <int EPI, bool I32>
+// rint(zp + t) for t = RN32(y / s) approximated by tf = RN32(y * RN32(1/s)) (|t - tf| <=
+// |tf| 2^-22.4): decided by tf when the rounding boundary is farther than |tf| 2^-21 (zp is
+// an integer, so zp + t rounds like t away from ties, and clipping to the integer bounds
+// commutes with rounding); else *slow is set and the caller recomputes exactly
+__device__ __forceinline__ int quant_filter(float tf, float zpf, float lof, float hif, bool* slow) {
+  const float r = __builtin_rintf(tf);
+  const float room = 0.5f - __builtin_fabsf(tf - r);
+  *slow = !(room > __builtin_fabsf(tf) * 0x1p-21f + 0x1p-126f);
+  return (int)__builtin_amdgcn_fmed3f(r + zpf, lof, hif);
+}
+
+// F32X (host-checked: |acc - zero-point term| < 2^24 for every element, |zp_out| <= 2^20):
+// the f32 dequantize (float)v * s_acc equals the f64 one (v and s_acc exact in f32, one
+// rounding), so the QKV and GELU epilogues run in f32 with rounding filters.
+template <int EPI, bool I32, bool F32X>
 __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, int N, const EpiCol4& c, v4i a,
                                          float4 r) {
   float d[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) d[k] = (EPI == EPI_GELU) ? 0.0f : dequant_elem<I32>(a[k], c.colterm[k], c.s_acc);
+  for (int k = 0; k < 4; ++k)
+    d[k] = (EPI == EPI_GELU || (EPI == EPI_QKV && F32X)) ? 0.0f : dequant_elem<I32>(a[k], c.colterm[k], c.s_acc);
   if constexpr (EPI == EPI_RESID) {
     const int64_t o = (int64_t)gm * N + c.dd;
     float4 y;
@@ -250,14 +269,20 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
           else vi = (int32_t)__builtin_fmin(__builtin_fmax((double)((int64_t)a[k] - c.colterm[k]), -2147483520.0), 2147483520.0);
           const float df = (float)vi * c.s_acc;
           const float hf = c.bias[k] + df;
-          const float tf = gelu_fast(hf) * e.rsf;
+          const float tf = gelu_fast(hf) * c.rsf;
           const float r = __builtin_rintf(tf);
           const float room = 0.5f - __builtin_fabsf(tf - r);
-          const float err = __builtin_fmaf(__builtin_fabsf(hf), e.g_rel, e.g_abs) + __builtin_fabsf(tf) * 0x1p-22f;
-          slow[k] = !((room > err) & (err < 0.25f) & (__builtin_fabsf(hf) < 0x1p64f) &
-                      (vi < (1 << 24)) & (vi > -(1 << 24)));
+          if constexpr (F32X) {
+            // g_rel also covers the product's |tf| 2^-22 (|gelu(h)| <= |h|), and
+            // |s_out| <= 2^20 makes err > 0.5 for every |h| >= 2^64 (host)
+            slow[k] = !(room > __builtin_fmaf(__builtin_fabsf(hf), e.g_rel, e.g_abs));
+          } else {
+            const float err = __builtin_fmaf(__builtin_fabsf(hf), e.g_rel, e.g_abs) + __builtin_fabsf(tf) * 0x1p-22f;
+            slow[k] = !((room > err) & (err < 0.25f) & (__builtin_fabsf(hf) < 0x1p64f) &
+                        (vi < (1 << 24)) & (vi > -(1 << 24)));
+          }
           any_slow |= slow[k];
-          q[k] = (int)__builtin_fminf(__builtin_fmaxf(r + e.zpf, e.lof), e.hif);
+          q[k] = (int)__builtin_amdgcn_fmed3f(r + c.zpf, e.lof, e.hif);
         }
         if (__builtin_expect(__any(any_slow), 0)) {
 #pragma unroll
@@ -279,6 +304,23 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
           packed |= ((uint32_t)(q & 0xff)) << (8 * k);
         }
       }
+    } else if constexpr (F32X) {  // EPI_QKV, f32 with the rounding filter
+      int q[4];
+      float y[4];
+      bool slow[4], any_slow = false;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        y[k] = c.bias[k] + (float)(a[k] - (int32_t)c.colterm[k]) * c.s_acc;
+        q[k] = quant_filter(y[k] * c.rsf, c.zpf, e.lof, e.hif, &slow[k]);
+        any_slow |= slow[k];
+      }
+      if (__builtin_expect(__any(any_slow), 0)) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (slow[k]) q[k] = quant_zp_u(y[k], c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) packed |= ((uint32_t)(q[k] & 0xff)) << (8 * k);
     } else {  // EPI_QKV
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -441,153 +483,49 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
 }
 
 // ---------------------------------------------------------------------------------------
-// Projection GEMM (A [M][K] activations x constant weights Bt [N][K]), batch 1:
-// 128x256 tiles, 4 waves (1 x 4, 128x64 each = 4x2 tiles of v_mfma_i32_32x32x32_i8),
-// BK = 64, a 3-stage LDS ring (72 KiB -> two blocks per CU, so one block's epilogue
-// overlaps the other's MFMA loop) filled by global_load_lds_dwordx4 behind counted
-// vmcnt waits and raw s_barriers.  The LDS image is lane-linear per 1 KiB piece; the
-// conflict-free chunk swizzle is applied to the SOURCE address.  Needs K % 64 == 0
-// and precomputed weight column sums (zero-point COL term only).
+// Projection GEMMs (A [M][K] activations x constant weights Bt [N][K]), batch 1, on
+// v_mfma_i32_32x32x32_i8.  Every wave owns a 128 x 64 output block (4 x 2 tiles of
+// 32x32); BK = 64; the stages are filled by global_load_lds_dwordx4 (LDS-DMA, 1 KiB
+// pieces of 16 rows x 64 B, lane-linear LDS image, the conflict-free chunk swizzle applied
+// to the SOURCE address) behind counted vmcnt waits and raw s_barriers.  A lane's 32
+// k-bytes of one MFMA pair are contiguous (k chunk 2*half + s): integer sums do not depend
+// on the k order, as long as A and B use the same one.  Both need K % 64 == 0 and
+// precomputed weight column sums (zero-point COL term only).
+//   k_qgemm_big: 128x256 tiles, 4 waves, a 3-stage ring with one barrier per k-step, two
+//                blocks per CU (K % 192 == 0: the k loop is unrolled by the ring depth).
+//   k_qgemm_pp:  256x256 tiles, 8 waves in two groups of 4 that alternate roles every
+//                half k-step ("ping-pong"): while one group runs its 16 MFMAs on stage s,
+//                the other reads its stage-s fragments from LDS and issues its share of
+//                stage s+2, so each SIMD (one wave of each group) keeps its matrix pipe
+//                busy while the partner loads; a third fewer LDS-DMA bytes per MFMA.
 constexpr int GBN = 256, GBK = 64, GST = 3;
-
-// WR wave rows: 1 -> 128x256 tile, 4 waves (1x4), two blocks per CU;
-//               2 -> 256x256 tile, 8 waves (2x4), one block per CU.
-template <int WR>
-struct BigTile {
-  static constexpr int BM = 128 * WR, NW = 4 * WR;
-  static constexpr int STAGE = (BM + GBN) * GBK;   // 24 / 32 KiB
-  static constexpr int AP = BM * GBK / 1024 / NW;  // A pieces per wave per stage (2)
-  static constexpr int BP = GBN * GBK / 1024 / NW; // B pieces per wave per stage (4 / 2)
-  static constexpr int PW = AP + BP;               // glds per wave per stage (6 / 4)
-  static constexpr int RP = 64 / WR;               // epilogue rows per pass and wave
-};
+constexpr int G_RP = 32;                          // epilogue rows per pass and wave
+constexpr int BIG_LDS = GST * (128 + GBN) * GBK;  // 72 KiB (>= 4 waves' staging, 36 KiB)
+constexpr int PP_LDS = GST * (256 + GBN) * GBK;   // 96 KiB (>= 8 waves' staging, 72 KiB)
+// Diagnostic builds only (tools/gemm_diag.sh, never the shipped library): bit 1 = no
+// global loads in the k loop, 2 = no LDS fragment reads, 4 = no k-step barrier, 8 = no MFMA
+// (k_qgemm_big).
+#ifndef NQK_DIAG
+#define NQK_DIAG 0
+#endif
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int EPI, bool I32, int WR>
-__global__ void __launch_bounds__(256 * WR, 3 - WR)
-k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
-            int tiles_m, int tiles_n, Epi e) {
-  using C = BigTile<WR>;
-  constexpr int GBM = C::BM, GAP = C::AP, GBP = C::BP, GSTAGE = C::STAGE, RP = C::RP;
-  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
-  const int nwg = tiles_m * tiles_n;
-  int wg = blockIdx.x;
-  if (nwg >= 8) {
-    const int q = nwg / 8, r = nwg % 8, x = wg % 8;
-    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
-  }
-  const int tm = wg / tiles_n, tn = wg % tiles_n;
-  const int m0 = tm * GBM, n0 = tn * GBN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;  // 1 or 2 wave rows of 4 waves along N
-
-  // this lane's source row / chunk for each of its A and B pieces (1 KiB = 16 rows)
-  const int prow = lane >> 2, ppos = lane & 3;
-  const int8_t* asrc[GAP];
-  const int8_t* bsrc[GBP];
-#pragma unroll
-  for (int p = 0; p < GAP; ++p) {
-    const int row = (wave * GAP + p) * 16 + prow;
-    asrc[p] = A + (int64_t)min(m0 + row, M - 1) * lda + (ppos ^ ((row >> 2) & 3)) * 16;
-  }
-#pragma unroll
-  for (int p = 0; p < GBP; ++p) {
-    const int row = (wave * GBP + p) * 16 + prow;
-    bsrc[p] = Bt + (int64_t)min(n0 + row, N - 1) * ldb + (ppos ^ ((row >> 2) & 3)) * 16;
-  }
-  auto issue = [&](int st) {
-    int8_t* slot = lds + (st % GST) * GSTAGE;
-    const int k0 = st * GBK;
-#pragma unroll
-    for (int p = 0; p < GAP; ++p)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[p] + k0), (lds_ptr_t)(slot + (wave * GAP + p) * 1024), 16, 0, 0);
-#pragma unroll
-    for (int p = 0; p < GBP; ++p)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[p] + k0),
-                                       (lds_ptr_t)(slot + GBM * GBK + (wave * GBP + p) * 1024), 16, 0, 0);
-  };
-
-  v16i acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
-
-  // one barrier per k-step: after it every wave has finished reading slot (kt-1)%3,
-  // which the same step refills with stage kt+2 (glds spread between the MFMAs).  The
-  // last two steps issue nothing (peeled, so each step body is one basic block).
-  const int nk = K / GBK;
-  issue(0);
-  if (nk > 1) issue(1);
+// ---- epilogue of both projection GEMMs, staged through LDS (no longer read by the main
+// loop): each wave owns a G_RP x 72-int32 slice; 128 / G_RP passes of G_RP rows.  Read
+// back row-major, a lane takes 4 consecutive columns of one row, so bias / column terms
+// are per lane and the outputs leave as 4-byte (int8) or 16-byte (f32) stores.
+template <int EPI, bool I32, bool F32X>
+__device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], const Epi& e, int mw, int ncol0,
+                                              int M, int N, int wave, int lane) {
+  constexpr int RP = G_RP;
   const int r32 = lane & 31, half = lane >> 5;
-  auto kstep = [&](int kt, auto refill, auto drain) {
-    if constexpr (decltype(drain)::value) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    } else if constexpr (WR == 1) {
-      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");  // stage kt+1 may fly
-    } else {
-      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    const int8_t* sa = lds + (kt % GST) * GSTAGE;
-    const int8_t* sb = sa + GBM * GBK;
-    v4i fa[2][4], fb[2][2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[s][i] = *reinterpret_cast<const v4i*>(sa + swz64(wm * 128 + i * 32 + r32, 2 * s + half));
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[s][j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * s + half));
-    }
-    if constexpr (decltype(refill)::value) issue(kt + 2);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
-    // issue order: the 6 s=0 fragment reads, then the MFMAs with the s=1 reads and the
-    // next stage's glds spread between them
-    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-#pragma unroll
-    for (int g = 0; g < 6; ++g) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    if constexpr (decltype(refill)::value) {
-#pragma unroll
-      for (int g = 0; g < GAP + GBP; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  for (int kt = 0; kt + 2 < nk; ++kt) kstep(kt, T_{}, F_{});
-  if (nk >= 2) kstep(nk - 2, F_{}, F_{});
-  kstep(nk - 1, F_{}, T_{});
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  // ---- epilogue, staged through LDS (the ring is free after the last barrier): each
-  // wave owns an RP x 72-int32 slice (72 KiB in all); 128 / RP passes of RP rows.  Read
-  // back row-major, a lane takes 4 consecutive columns of one row, so bias / column
-  // terms are per lane and the outputs leave as 4-byte (int8) or 16-byte (f32) stores.
   int32_t* stg = reinterpret_cast<int32_t*>(lds) + wave * (RP * 72);
-  const int mw = m0 + wm * 128;
   const int c4 = (lane & 15) * 4;
-  const int gn0 = n0 + wn * 64 + c4;
+  const int gn0 = ncol0 + c4;
   const bool cok = gn0 < N;  // N % 4 == 0 (host-checked): the 4 columns are valid together
   EpiCol4 cc = epi_col4<EPI>(e, gn0, cok);
 #pragma unroll
@@ -619,7 +557,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     auto row_step = [&](int it, float4 r4) {
       const int rl = it * 4 + (lane >> 4);
       const v4i a4 = *reinterpret_cast<const v4i*>(stg + rl * 72 + c4);
-      if (gm < M && cok) epi_row4<EPI, I32>(e, gm, img, t, N, cc, a4, r4);
+      if (gm < M && cok) epi_row4<EPI, I32, F32X>(e, gm, img, t, N, cc, a4, r4);
       gm += 4;
       if constexpr (EPI == EPI_QKV) {
         t += 4;
@@ -635,6 +573,275 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     }
     wave_lds_sync();
   }
+}
+
+// XCD-aware tile order: XCD x (= blockIdx % 8) walks one contiguous band of tiles, so
+// the blocks that share an A row panel share one L2
+#ifndef NQK_TILE_ORDER
+#define NQK_TILE_ORDER 0  // diagnostic builds: 1 = plain block order, 2 = column-panel bands
+#endif
+__device__ __forceinline__ int xcd_tile(int nwg) {
+  int wg = blockIdx.x;
+  if (NQK_TILE_ORDER != 1 && nwg >= 8) {
+    const int q = nwg / 8, r = nwg % 8, x = wg % 8;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
+  }
+  return wg;
+}
+// tile (tm, tn) of tile id wg: row-panel-major (blocks with consecutive ids share A rows)
+__device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& tm, int& tn) {
+  if (NQK_TILE_ORDER == 2) {
+    tn = wg / tiles_m;
+    tm = wg - tn * tiles_m;
+  } else {
+    tm = wg / tiles_n;
+    tn = wg - tm * tiles_n;
+  }
+}
+
+template <int EPI, bool I32, bool F32X>
+__global__ void __launch_bounds__(256, 2)
+k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
+            int tiles_m, int tiles_n, Epi e) {
+  constexpr int GBM = 128;
+  constexpr int AP = GBM * GBK / 1024 / 4;  // A pieces per wave per stage (2)
+  constexpr int BP = GBN * GBK / 1024 / 4;  // B pieces per wave per stage (4)
+  constexpr int PW = AP + BP;               // LDS-DMA ops per wave per stage (6)
+  constexpr int STAGE = (GBM + GBN) * GBK;  // 24 KiB
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  int tm, tn;
+  tile_of(xcd_tile(tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave;  // 4 waves along N
+  const int r32 = lane & 31, half = lane >> 5;
+
+  // LDS-DMA sources: this lane's row / chunk for each 1 KiB piece (16 rows x 64 B)
+  const int prow = lane >> 2, ppos = lane & 3;
+  const int8_t* asrc[AP];
+  const int8_t* bsrc[BP];
+#pragma unroll
+  for (int p = 0; p < AP; ++p) {
+    const int row = (wave * AP + p) * 16 + prow;
+    asrc[p] = A + (int64_t)min(m0 + row, M - 1) * lda + (ppos ^ ((row >> 2) & 3)) * 16;
+  }
+#pragma unroll
+  for (int p = 0; p < BP; ++p) {
+    const int row = (wave * BP + p) * 16 + prow;
+    bsrc[p] = Bt + (int64_t)min(n0 + row, N - 1) * ldb + (ppos ^ ((row >> 2) & 3)) * 16;
+  }
+  auto issue = [&](int st, auto SLOT) {
+    constexpr int sl = decltype(SLOT)::value;
+    if constexpr ((NQK_DIAG & 1) != 0) return;
+    int8_t* slot = lds + sl * STAGE;
+    const int k0 = st * GBK;
+#pragma unroll
+    for (int p = 0; p < AP; ++p)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[p] + k0), (lds_ptr_t)(slot + (wave * AP + p) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < BP; ++p)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[p] + k0),
+                                       (lds_ptr_t)(slot + GBM * GBK + (wave * BP + p) * 1024), 16, 0, 0);
+  };
+
+  v16i acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+
+  // one barrier per k-step: after it every wave has finished reading slot (kt-1)%3,
+  // which the same step refills with stage kt+2 (loads spread between the MFMAs)
+  auto kstep = [&](int kt, auto SLOT, auto refill, auto drain) {
+    constexpr int sl = decltype(SLOT)::value;
+    if constexpr (decltype(drain)::value) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");  // stage kt+1 may fly
+    }
+    if constexpr ((NQK_DIAG & 4) == 0) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int8_t* sa = lds + sl * STAGE;
+    const int8_t* sb = sa + GBM * GBK;
+    v4i fa[2][4], fb[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if constexpr ((NQK_DIAG & 2) != 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[s][i] = v4i{kt + i, lane, s, 1};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[s][j] = v4i{kt + j, lane, s, 2};
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[s][i] = *reinterpret_cast<const v4i*>(sa + swz64(i * 32 + r32, 2 * half + s));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[s][j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * half + s));
+    }
+    if constexpr (decltype(refill)::value) issue(kt + 2, std::integral_constant<int, (sl + 2) % GST>{});
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if constexpr ((NQK_DIAG & 8) == 0)
+            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j][0] ^= fa[s][i][0] ^ fb[s][j][1];
+        }
+    // issue order: the s=0 fragment reads, then the MFMAs with the s=1 reads and the
+    // next stage's loads spread between them
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    if constexpr (decltype(refill)::value) {
+#pragma unroll
+      for (int g = 0; g < PW; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 10 - (decltype(refill)::value ? PW : 0), 0);
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  const int nk = K / GBK;  // a multiple of 3 (host-checked): the ring slot of step kt is kt % 3
+  issue(0, S0{});
+  issue(1, S1{});
+  for (int kt = 0; kt + 3 < nk; kt += 3) {  // every step refills (stage kt + 4 < nk)
+    kstep(kt, S0{}, T_{}, F_{});
+    kstep(kt + 1, S1{}, T_{}, F_{});
+    kstep(kt + 2, S2{}, T_{}, F_{});
+  }
+  kstep(nk - 3, S0{}, T_{}, F_{});
+  kstep(nk - 2, S1{}, F_{}, F_{});
+  kstep(nk - 1, S2{}, F_{}, T_{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  proj_epilogue<EPI, I32, F32X>(lds, acc, e, m0, n0 + wn * 64, M, N, wave, lane);
+}
+
+template <int EPI, bool I32, bool F32X>
+__global__ void __launch_bounds__(512, 1)
+k_qgemm_pp(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
+           int tiles_m, int tiles_n, Epi e) {
+  constexpr int BM = 256;
+  constexpr int STAGE = (BM + GBN) * GBK;  // 32 KiB
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  int tm, tn;
+  tile_of(xcd_tile(tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * GBN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar branches
+  const int grp = wave >> 2, wn = wave & 3;
+  const int r32 = lane & 31, half = lane >> 5;
+
+  // LDS-DMA: each wave moves 2 A and 2 B pieces (16 rows x 64 B) of every stage
+  const int prow = lane >> 2, ppos = lane & 3;
+  const int8_t* asrc[2];
+  const int8_t* bsrc[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int row = (wave * 2 + p) * 16 + prow;  // 0..255
+    const int sw = (ppos ^ ((row >> 2) & 3)) * 16;
+    asrc[p] = A + (int64_t)min(m0 + row, M - 1) * lda + sw;
+    bsrc[p] = Bt + (int64_t)min(n0 + row, N - 1) * ldb + sw;
+  }
+  auto issue = [&](int st, int slot) {
+    int8_t* sl = lds + slot * STAGE;
+    const int k0 = st * GBK;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[p] + k0), (lds_ptr_t)(sl + (wave * 2 + p) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[p] + k0),
+                                       (lds_ptr_t)(sl + BM * GBK + (wave * 2 + p) * 1024), 16, 0, 0);
+  };
+
+  v16i acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+  v4i fa[2][4], fb[2][2];
+  const int nk = K / GBK;
+  // load segment: this wave's fragments of stage st from its slot, then its share of
+  // stage st+2 into slot (st+2) % 3 (last read two half-steps ago); lgkmcnt(0) before the
+  // barrier that ends the segment (fragments in registers, slot reads retired)
+  auto load_seg = [&](int st, int slot) {
+    const int8_t* sa = lds + slot * STAGE;
+    const int8_t* sb = sa + BM * GBK;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[s][i] = *reinterpret_cast<const v4i*>(sa + swz64(grp * 128 + i * 32 + r32, 2 * half + s));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[s][j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * half + s));
+    }
+    if (st + 2 < nk) issue(st + 2, slot == 0 ? 2 : slot - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  // compute segment: 16 MFMAs on the fragments of the last load segment; s_setprio keeps
+  // the cluster between its barriers and ahead of the partner's loads on the SIMD
+  auto compute_seg = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+  };
+  // stage st+1 complete for this wave: after each segment, the wave's own pieces of the
+  // stage after the one it reads next have landed (at most stage st+2's 4 in flight)
+  auto wait_next = [&](int st) {
+    if (st + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  wait_next(-1);
+  barrier();
+  // the stagger: group 1 runs one half-step behind group 0, so in every barrier interval
+  // one group loads while the other computes; both run the same segment sequence
+  if (grp == 1) barrier();
+  int slot = 0;
+  for (int st = 0; st < nk; ++st) {
+    load_seg(st, slot);
+    wait_next(st);
+    barrier();
+    compute_seg();
+    wait_next(st);
+    barrier();
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  if (grp == 0) barrier();  // same barrier count for both groups
+  // every load segment ended (lgkmcnt(0)) before the last barrier: the ring is free
+  proj_epilogue<EPI, I32, F32X>(lds, acc, e, m0 + grp * 128, n0 + wn * 64, M, N, wave, lane);
 }
 
 // ------------------------------------------------------------------ LayerNorm + quantize
@@ -827,14 +1034,26 @@ k_transpose_pad(const int8_t* __restrict__ src, int8_t* __restrict__ dst, int64_
 
 using namespace nqk;
 
-// projection tile: NQK_BIG_TILE=256 selects the 256x256 / 8-wave variant (read once)
-static int big_tile_rows() {
-  static int wr = 0;
-  if (!wr) {
-    const char* v = getenv("NQK_BIG_TILE");
-    wr = (v && atoi(v) == 256) ? 2 : 1;
+// projection GEMM kernel: the 128x256 one; NQK_GEMM_PP=1 selects the ping-pong 256x256
+// one (measured no faster: the k loop is bound by the LDS-DMA latency, not the issue)
+static bool gemm_pingpong() {
+  const char* v = getenv("NQK_GEMM_PP");
+  return v && atoi(v) == 1;
+}
+
+template <int EPI, bool I32, bool F32X>
+static void launch_big(bool pp, const int8_t* a, const int8_t* bt, int64_t M, int64_t N, int64_t K, int64_t lda,
+                       int64_t ldb, const Epi& e) {
+  const int tn = (int)((N + GBN - 1) / GBN);
+  if (pp) {
+    const int tm = (int)((M + 255) / 256);
+    hipLaunchKernelGGL((k_qgemm_pp<EPI, I32, F32X>), dim3(tm * tn), dim3(512), PP_LDS, stream(), a, bt, (int)M,
+                       (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e);
+  } else {
+    const int tm = (int)((M + 127) / 128);
+    hipLaunchKernelGGL((k_qgemm_big<EPI, I32, F32X>), dim3(tm * tn), dim3(256), BIG_LDS, stream(), a, bt, (int)M,
+                       (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e);
   }
-  return wr;
 }
 
 static Epi make_epi(const nqk_epilogue* p) {
@@ -867,13 +1086,17 @@ static Epi make_epi(const nqk_epilogue* p) {
   // the GELU filter's bound is proven for these constants only (nqk_selftest_gelu_filter)
   e.gelu_filter = p->div == 1.41421354f && p->add1 == 1.0f && p->mul2 == 0.5f && p->zp_out[0] >= -(1 << 20) &&
                   p->zp_out[0] <= (1 << 20) && __builtin_fabsf(p->s_out[0]) >= 0x1p-60f &&
-                  __builtin_fabsf(p->s_out[0]) <= 0x1p60f && !(getenv("NQK_NO_GELU_FILTER"));
-  e.rsf = (float)(1.0 / (double)p->s_out[0]);
-  // |d(gelu)/dh| <= 1.13, so an h error of |d| 2^-23 moves y by at most |d| 2^-22.8
+                  __builtin_fabsf(p->s_out[0]) <= 0x1p20f && !(getenv("NQK_NO_GELU_FILTER"));
+  for (int g = 0; g < 3; ++g) {
+    e.rsf[g] = (p->s_out[g] != 0.0f) ? (float)(1.0 / (double)p->s_out[g]) : 0.0f;
+    e.zpf[g] = (float)p->zp_out[g];
+  }
+  // GELU filter error in units of t: |gelu_fast - gelu| <= GELU_REL |h| + GELU_ABS, and
+  // the product t = y * rsf adds |t| 2^-22 <= |h| |1/s| 2^-21.9 (|gelu(h)| <= |h|), i.e.
+  // 0.27 GELU_REL |h| |1/s| at most; 2 % margin on 1/s
   const double ars = __builtin_fabs(1.0 / (double)p->s_out[0]) * 1.02;
-  e.g_rel = (float)(GELU_REL * ars);
+  e.g_rel = (float)((double)GELU_REL * 1.27 * ars);
   e.g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
-  e.zpf = (float)p->zp_out[0];
   e.lof = (float)e.lo;
   e.hif = (float)e.hi;
   return e;
@@ -899,7 +1122,8 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   const double kk = (double)(params->kdim > K ? params->kdim : K);
   const double bound = 16384.0 * kk + 128.0 * kk * (za + zb) + za * zb * kk;
   const bool i32 = bound < 2147483647.0 * 0.98;
-  const bool big = batch == 1 && (K % GBK) == 0 && (N % 4) == 0 && params->zp_flags == NQK_ZP_COL &&
+  const bool pp = gemm_pingpong();
+  const bool big = batch == 1 && (K % (pp ? GBK : GST * GBK)) == 0 && K > 0 && (N % 4) == 0 && params->zp_flags == NQK_ZP_COL &&
                    params->col != nullptr && (epi != EPI_QKV || (params->hdim % 4 == 0 && params->group_cols % 4 == 0)) &&
                    (epi == EPI_QKV || epi == EPI_RESID || epi == EPI_GELU || epi == EPI_NULL);
   // staged epilogue stores 4 columns at once: 16-byte (f32) / 4-byte (int8) aligned outputs
@@ -911,23 +1135,23 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   if (epi == EPI_QKV) scales_ok = normal(params->s_out[0]) && normal(params->s_out[1]) && normal(params->s_out[2]);
   if (epi == EPI_GELU) scales_ok = scales_ok && normal(params->div);
   if (big && aligned && scales_ok) {
-    const int wr = big_tile_rows();
-    const int bm = 128 * wr;
-    const int tm = (int)((M + bm - 1) / bm), tn = (int)((N + GBN - 1) / GBN);
-    const size_t shm = (size_t)GST * (wr == 1 ? BigTile<1>::STAGE : BigTile<2>::STAGE);
-    switch (epi * 4 + (i32 ? 2 : 0) + (wr - 1)) {
+    // f32 epilogue arithmetic when every |acc - col term| < 2^24 (int8 operands:
+    // |acc| <= 2^14 K) and the output zero points are exact in f32 with room to spare
+    const double cmax = params->col_absmax > 0 ? (double)params->col_absmax : 128.0 * (double)K;
+    const int ng = epi == EPI_QKV ? 3 : 1;
+    bool zp_small = true;
+    for (int g = 0; g < ng; ++g) zp_small = zp_small && params->zp_out[g] >= -(1 << 20) && params->zp_out[g] <= (1 << 20);
+    const bool f32x = i32 && (epi == EPI_QKV || epi == EPI_GELU) && zp_small &&
+                      16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
+    switch (epi * 3 + (f32x ? 2 : (i32 ? 1 : 0))) {
 #define LB(E) \
-      case E * 4 + 0: hipLaunchKernelGGL((k_qgemm_big<E, false, 1>), dim3(tm * tn), dim3(256), shm, stream(), a, bt, \
-                                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break; \
-      case E * 4 + 1: hipLaunchKernelGGL((k_qgemm_big<E, false, 2>), dim3(tm * tn), dim3(512), shm, stream(), a, bt, \
-                                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break; \
-      case E * 4 + 2: hipLaunchKernelGGL((k_qgemm_big<E, true, 1>), dim3(tm * tn), dim3(256), shm, stream(), a, bt, \
-                                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break; \
-      case E * 4 + 3: hipLaunchKernelGGL((k_qgemm_big<E, true, 2>), dim3(tm * tn), dim3(512), shm, stream(), a, bt, \
-                                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e); break;
+      case E * 3 + 0: launch_big<E, false, false>(pp, a, bt, M, N, K, lda, ldb, e); break; \
+      case E * 3 + 1: launch_big<E, true, false>(pp, a, bt, M, N, K, lda, ldb, e); break;
       LB(EPI_QKV) LB(EPI_RESID) LB(EPI_GELU) LB(EPI_NULL)
 #undef LB
-      default: break;
+      case EPI_QKV * 3 + 2: launch_big<EPI_QKV, true, true>(pp, a, bt, M, N, K, lda, ldb, e); break;
+      case EPI_GELU * 3 + 2: launch_big<EPI_GELU, true, true>(pp, a, bt, M, N, K, lda, ldb, e); break;
+      default: return fail("nqk_qgemm_fused: no big-tile kernel for this epilogue");
     }
     return launch_status("nqk_qgemm_fused(big)");
   }

@@ -27,7 +27,7 @@ class Epilogue(ctypes.Structure):
     """Mirror of `nqk_epilogue` (include/nqk.h)."""
     _fields_ = [("zp_flags", ctypes.c_int32), ("bit_width", ctypes.c_int32), ("group_cols", ctypes.c_int32),
                 ("tokens", ctypes.c_int32), ("heads", ctypes.c_int32), ("hdim", ctypes.c_int32),
-                ("ld_out", ctypes.c_int32), ("pad0", ctypes.c_int32),
+                ("ld_out", ctypes.c_int32), ("col_absmax", ctypes.c_int32),
                 ("zpa", ctypes.c_int64), ("zpb", ctypes.c_int64), ("kdim", ctypes.c_int64),
                 ("row", ctypes.c_void_p), ("col", ctypes.c_void_p),
                 ("s_acc", ctypes.c_float * 3), ("s_out", ctypes.c_float * 3), ("zp_out", ctypes.c_int64 * 3),

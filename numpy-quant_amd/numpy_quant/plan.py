@@ -458,6 +458,9 @@ class FusedLayer:
         self.s_wo, self.s_w1, self.s_w2 = m.wo.data.scale, m.w1.data.scale, m.w2.data.scale
         self.bias_o, self.bias_1, self.bias_2 = deq(m.bo).dev, deq(m.b1).dev, deq(m.b2).dev
         self.F = self.bt_1.shape[0]
+        # max |column sum| of each weight: lets the GEMM epilogues prove f32 exactness
+        self.cmax = {k: _absmax(c) for k, c in (("qkv", self.col_qkv), ("o", self.col_o), ("1", self.col_1),
+                                                 ("2", self.col_2))}
         if self.D != m.heads * m.hdim or self.bt_o.shape != (self.D, self.D) or self.bt_2.shape != (self.D, self.F):
             raise NoMatch("layer dimensions")
         # the one-kernel attention covers head size 64, <= 224 tokens and zero points for
@@ -518,6 +521,7 @@ class FusedLayer:
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D, col=self.col_qkv.ptr,
+                      col_absmax=self.cmax["qkv"],
                       s_acc=[_f32(s_a * np.float32(self.s_w[r])) for r in "qkv"],
                       s_out=[_f32(self.p_head[r].scale) for r in "qkv"],
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
@@ -541,25 +545,31 @@ class FusedLayer:
             self._attention_unfused(w, B, T, Tp, H, Dh, D)
         # 7) output projection + bias + residual
         x1 = DeviceArray((B, T, D), np.float32)
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr,
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr, col_absmax=self.cmax["o"],
                       s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
                       resid=x.dev.ptr, out=[x1.ptr])
         _gemm(EPI_RESID, w["ctx"], self.bt_o, 1, Mrows, D, D, D, D, None, 0, 0, e)
         # 8) LN2 + quantize
         _ln_quant(x1, self.g2, self.be2, w["ln2q"], Mrows, D, self.eps2, self.p_ln2, bw)
         # 9) FFN up + bias + GELU + quantize
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr,
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr, col_absmax=self.cmax["1"],
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
                       s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[w["h"].ptr],
                       div=m.gelu_div, add1=m.gelu_add, mul2=m.gelu_mul)
         _gemm(EPI_GELU, w["ln2q"], self.bt_1, 1, Mrows, F, D, D, D, None, 0, 0, e)
         # 10) FFN down + bias + residual
         x2 = DeviceArray((B, T, D), np.float32)
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr,
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr, col_absmax=self.cmax["2"],
                       s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
                       resid=x1.ptr, out=[x2.ptr])
         _gemm(EPI_RESID, w["h"], self.bt_2, 1, Mrows, D, F, F, F, None, 0, 0, e)
         m.x_out.data = FTensor(x2)
+
+
+def _absmax(col) -> int:
+    """max |column sum| (int32-clamped; 0 would mean unknown to the kernel, so >= 1)."""
+    v = int(np.abs(col.to_host()).max()) if col.size else 1
+    return max(1, min(v, 2 ** 31 - 1))
 
 
 def _ln_quant(x, g, b, out, rows, cols, eps, p, bw):

@@ -87,3 +87,68 @@ def test_patchify_dequant_equals_dequantize_then_im2col(n, c, h, w, kh, kw, zp):
     cols = DeviceArray(ref_cols.shape, np.float32)
     _lib.call("nqk_patchify_dequant", DeviceArray.from_host(q).vp, cols.vp, n, c, h, w, kh, kw, float(s), zp)
     np.testing.assert_array_equal(cols.to_host(), ref_cols.to_host())
+
+
+_VARIANTS = [{}, {"NQK_GEMM_PP": "1"}, {"NQK_NO_F32X": "1"}, {"NQK_NO_F32X": "1", "NQK_GEMM_PP": "1"},
+             {"NQK_NO_GELU_FILTER": "1", "NQK_NO_F32X": "1"}]
+
+
+@pytest.mark.parametrize("epi_name,M,N,K,zpa,s_out,zp", [
+    ("qkv", 4 * 197, 2304, 768, -7, (0.021, 0.0173, 0.05), (3, -140, 0)),
+    ("qkv", 2 * 197, 2304, 192, 131, (0.9, 0.0011, 2.5e-3), (0, 17, -3)),
+    ("resid", 1024 + 77, 772, 768, 5, (1, 1, 1), (0, 0, 0)),
+    ("resid", 512, 768, 3072, -120, (1, 1, 1), (0, 0, 0)),
+    ("gelu", 1024 + 77, 3072, 768, -3, (0.0027, 1, 1), (-9, 0, 0)),
+    ("gelu", 300, 772, 192, 140, (0.05, 1, 1), (2, 0, 0)),
+    ("resid", 77, 256, 192, 3, (1, 1, 1), (0, 0, 0)),
+    ("gelu", 513, 512, 1536, -1, (0.02, 1, 1), (0, 0, 0)),
+])
+def test_projection_gemm_variants_agree(epi_name, M, N, K, zpa, s_out, zp, monkeypatch):
+    """Projection GEMM variants: the ping-pong 256x256 kernel (k_qgemm_pp) or the 128x256
+    one (k_qgemm_big), f64 or proven-exact f32 epilogue arithmetic with rounding filters,
+    GELU filter on or off -- all bit-identical, on ragged tiles and small output scales
+    that put many values next to rounding boundaries.  The exact-chain variant is itself
+    checked against the reference's node loop by the plan tests."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_GELU, EPI_QKV, EPI_RESID, _gemm
+    epi = {"qkv": EPI_QKV, "resid": EPI_RESID, "gelu": EPI_GELU}[epi_name]
+    rng = np.random.default_rng(M + N + K + zpa)
+    a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
+    bt_h = rng.integers(-24, 25, size=(N, K), dtype=np.int8)
+    bt = DeviceArray.from_host(bt_h)
+    col_h = bt_h.astype(np.int64).sum(axis=1)
+    col = DeviceArray.from_host(col_h)
+    bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
+    resid = DeviceArray.from_host(rng.standard_normal((M, N)).astype(np.float32))
+    outs = []
+    for var in _VARIANTS:
+        for k in ("NQK_GEMM_PP", "NQK_NO_F32X", "NQK_NO_GELU_FILTER"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in var.items():
+            monkeypatch.setenv(k, v)
+        e = _lib.Epilogue()
+        e.zp_flags, e.bit_width = _lib.ZP_COL, 8
+        e.zpa, e.col, e.col_absmax = zpa, col.ptr, int(np.abs(col_h).max())
+        e.bias = bias.ptr
+        if epi == EPI_QKV:
+            T, H, Dh = 197, N // 3 // 64, 64
+            e.group_cols, e.tokens, e.heads, e.hdim = N // 3, T, H, Dh
+            bufs = [DeviceArray((M // T * H * T, Dh), np.int8) for _ in range(3)]
+            for g in range(3):
+                e.s_acc[g] = float(np.float32(1.7e-4 * (g + 1)))
+                e.s_out[g], e.zp_out[g], e.out[g] = s_out[g], zp[g], bufs[g].ptr
+        elif epi == EPI_RESID:
+            e.group_cols = 1 << 30
+            bufs = [DeviceArray((M, N), np.float32)]
+            e.s_acc[0], e.out[0], e.resid = float(np.float32(3.1e-4)), bufs[0].ptr, resid.ptr
+        else:
+            e.group_cols = 1 << 30
+            bufs = [DeviceArray((M, N), np.int8)]
+            e.s_acc[0], e.s_out[0], e.zp_out[0], e.out[0] = float(np.float32(1.3e-4)), s_out[0], zp[0], bufs[0].ptr
+            e.div, e.add1, e.mul2 = float(np.float32(1.4142135381698608)), 1.0, 0.5
+        _gemm(epi, a, bt, 1, M, N, K, K, K, None, 0, 0, e)
+        outs.append([b.to_host() for b in bufs])
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            np.testing.assert_array_equal(x, y)

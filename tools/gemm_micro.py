@@ -12,6 +12,8 @@ sys.path.insert(0, os.path.join(ROOT, "numpy-quant_amd"))
 from numpy_quant import _lib  # noqa: E402
 from numpy_quant.device import DeviceArray  # noqa: E402
 
+if os.environ.get("GM_LIB"):  # a diagnostic build (tools/gemm_diag.sh)
+    _lib.LIB_PATH = os.environ["GM_LIB"]
 _lib.ensure_init()
 M = int(os.environ.get("GM_M", 256 * 197))
 shapes = {"qkv": (2304, 768, 0), "out": (768, 768, 3), "up": (3072, 768, 4), "down": (768, 3072, 3)}
