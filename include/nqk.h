@@ -200,7 +200,8 @@ typedef struct nqk_epilogue {
   void* out[3];                         /* outputs per column group                     */
   const float* bias;                    /* dequantized bias [N] (EPI_QKV/RESID/GELU)    */
   const float* resid;                   /* residual [M][N] (EPI_RESID)                  */
-  float div, add1, mul2, pad1;          /* Div constant (8 / sqrt 2), GELU +1 and *0.5  */
+  float div, add1, mul2;                /* Div constant (8 / sqrt 2), GELU +1 and *0.5  */
+  int32_t b_packed;                     /* bt is the nqk_pack_b image of the weight      */
 } nqk_epilogue;
 /* int8 MFMA GEMM C = A . Bt^T (layouts as nqk_qgemm_i8) with a fused epilogue:
  *   QKV    model.py MatMul -> Add(bias) -> Reshape -> Transpose -> quantize, 3 groups
@@ -208,6 +209,12 @@ typedef struct nqk_epilogue {
  *   PV     MatMul(P, V) -> Transpose -> Reshape -> quantize      -> int8
  *   RESID  MatMul -> Add(bias) -> Add(residual)                  -> f32
  *   GELU   MatMul -> Add(bias) -> Div -> Erf -> Add -> Mul -> Mul -> quantize */
+/* Tile-packed copy of a constant int8 weight operand Bt [N][K] (K % 64 == 0) for
+ * nqk_qgemm_fused with b_packed = 1: [ceil(N/256)][K/64] blocks of 256 rows x 64 bytes in
+ * the GEMM's LDS stage image (zero rows past N); out holds ceil(N/256)*256*K bytes.  The packed
+ * operand is read as whole 128-byte lines (replaces no reference function: a layout of
+ * the same numpy_quantization.py:44-61 q_matmul operand). */
+int nqk_pack_b(const int8_t* bt, int8_t* out, int64_t N, int64_t K, int64_t ldb);
 int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, int64_t M, int64_t N, int64_t K,
                     int64_t lda, int64_t ldb, const int64_t* bmap, int64_t a_mat_stride, int64_t b_mat_stride,
                     const nqk_epilogue* params);

@@ -77,6 +77,7 @@ struct Epi {
   float rsf[3], zpf[3];      // f32 RN(1/s_out), zp_out per group, for the rounding filters
   float lof, hif;            // lo, hi as f32
   float g_rel, g_abs;        // GELU filter error terms, in units of t
+  int b_packed;              // Bt is the tile-packed image of nqk_pack_b
 };
 
 enum { EPI_QKV = 0, EPI_SCORES = 1, EPI_PV = 2, EPI_RESID = 3, EPI_GELU = 4, EPI_NULL = 5 };
@@ -625,22 +626,28 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     const int row = (wave * AP + p) * 16 + prow;
     asrc[p] = A + (int64_t)min(m0 + row, M - 1) * lda + (ppos ^ ((row >> 2) & 3)) * 16;
   }
+  // B: row-major Bt, or the tile-packed image of nqk_pack_b (every LDS-DMA piece one
+  // contiguous KiB = eight full 128-B lines, the swizzle already applied)
+  const bool bpk = e.b_packed != 0;
+  const int64_t bstep = bpk ? (int64_t)GBN * GBK : GBK;
 #pragma unroll
   for (int p = 0; p < BP; ++p) {
     const int row = (wave * BP + p) * 16 + prow;
-    bsrc[p] = Bt + (int64_t)min(n0 + row, N - 1) * ldb + (ppos ^ ((row >> 2) & 3)) * 16;
+    bsrc[p] = bpk ? Bt + (int64_t)tn * (K / GBK) * (GBN * GBK) + (wave * BP + p) * 1024 + lane * 16
+                  : Bt + (int64_t)min(n0 + row, N - 1) * ldb + (ppos ^ ((row >> 2) & 3)) * 16;
   }
   auto issue = [&](int st, auto SLOT) {
     constexpr int sl = decltype(SLOT)::value;
     if constexpr ((NQK_DIAG & 1) != 0) return;
     int8_t* slot = lds + sl * STAGE;
     const int k0 = st * GBK;
+    const int64_t kb = st * bstep;
 #pragma unroll
     for (int p = 0; p < AP; ++p)
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[p] + k0), (lds_ptr_t)(slot + (wave * AP + p) * 1024), 16, 0, 0);
 #pragma unroll
     for (int p = 0; p < BP; ++p)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[p] + k0),
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[p] + kb),
                                        (lds_ptr_t)(slot + GBM * GBK + (wave * BP + p) * 1024), 16, 0, 0);
   };
 
@@ -842,6 +849,24 @@ k_qgemm_pp(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, i
   if (grp == 0) barrier();  // same barrier count for both groups
   // every load segment ended (lgkmcnt(0)) before the last barrier: the ring is free
   proj_epilogue<EPI, I32, F32X>(lds, acc, e, m0 + grp * 128, n0 + wn * 64, M, N, wave, lane);
+}
+
+// Tile-packed image of a constant weight operand Bt [N][K] for k_qgemm_big: for column
+// panel tn (256 rows, zero padded past N) and k-step kt (64 bytes), one 16 KiB block whose
+// byte row*64 + pos*16 + b holds Bt[tn*256 + row][kt*64 + (pos ^ ((row >> 2) & 3))*16 + b]:
+// the lane-linear LDS image of the stage, so each LDS-DMA piece is one contiguous KiB.
+__global__ void k_pack_b(const int8_t* __restrict__ bt, int8_t* __restrict__ out, int64_t N, int64_t K, int64_t ldb,
+                         int64_t chunks) {
+  const int64_t nk = K / GBK;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < chunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t blk = c >> 10, w = c & 1023;  // 1024 16-B chunks per 16 KiB block
+    const int64_t tn = blk / nk, kt = blk - tn * nk;
+    const int row = (int)(w >> 2), pos = (int)(w & 3);
+    const int64_t n = tn * GBN + row;
+    v4i v = {0, 0, 0, 0};
+    if (n < N) v = *reinterpret_cast<const v4i*>(bt + n * ldb + kt * GBK + ((pos ^ ((row >> 2) & 3)) << 4));
+    *reinterpret_cast<v4i*>(out + c * 16) = v;
+  }
 }
 
 // ------------------------------------------------------------------ LayerNorm + quantize
@@ -1097,9 +1122,21 @@ static Epi make_epi(const nqk_epilogue* p) {
   const double ars = __builtin_fabs(1.0 / (double)p->s_out[0]) * 1.02;
   e.g_rel = (float)((double)GELU_REL * 1.27 * ars);
   e.g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
+  e.b_packed = p->b_packed;
   e.lof = (float)e.lo;
   e.hif = (float)e.hi;
   return e;
+}
+
+static int64_t pack_b_bytes(int64_t N, int64_t K) { return (N + GBN - 1) / GBN * GBN * K; }
+
+extern "C" int nqk_pack_b(const int8_t* bt, int8_t* out, int64_t N, int64_t K, int64_t ldb) {
+  if (N <= 0 || K <= 0) return 0;
+  if (K % GBK) return fail("nqk_pack_b: K must be a multiple of 64");
+  if ((((uintptr_t)bt) & 15) || (ldb & 15) || (((uintptr_t)out) & 15)) return fail("nqk_pack_b: unaligned operand");
+  const int64_t chunks = pack_b_bytes(N, K) / 16;
+  hipLaunchKernelGGL(k_pack_b, dim3(grid_for(chunks)), dim3(kThreads), 0, stream(), bt, out, N, K, ldb, chunks);
+  return launch_status("nqk_pack_b");
 }
 
 extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, int64_t M, int64_t N,
@@ -1134,6 +1171,9 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   bool scales_ok = normal(params->s_out[0]) || epi == EPI_RESID || epi == EPI_NULL;
   if (epi == EPI_QKV) scales_ok = normal(params->s_out[0]) && normal(params->s_out[1]) && normal(params->s_out[2]);
   if (epi == EPI_GELU) scales_ok = scales_ok && normal(params->div);
+  if (params->b_packed && !(big && aligned && scales_ok && (K % (GST * GBK)) == 0))
+    return fail("nqk_qgemm_fused: a packed B operand needs the big-tile path (K % 192 == 0, N % 4 == 0, "
+                "COL zero-point term, aligned outputs)");
   if (big && aligned && scales_ok) {
     // f32 epilogue arithmetic when every |acc - col term| < 2^24 (int8 operands:
     // |acc| <= 2^14 K) and the output zero points are exact in f32 with room to spare
@@ -1143,14 +1183,15 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     for (int g = 0; g < ng; ++g) zp_small = zp_small && params->zp_out[g] >= -(1 << 20) && params->zp_out[g] <= (1 << 20);
     const bool f32x = i32 && (epi == EPI_QKV || epi == EPI_GELU) && zp_small &&
                       16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
+    const bool use_pp = pp && !params->b_packed;
     switch (epi * 3 + (f32x ? 2 : (i32 ? 1 : 0))) {
 #define LB(E) \
-      case E * 3 + 0: launch_big<E, false, false>(pp, a, bt, M, N, K, lda, ldb, e); break; \
-      case E * 3 + 1: launch_big<E, true, false>(pp, a, bt, M, N, K, lda, ldb, e); break;
+      case E * 3 + 0: launch_big<E, false, false>(use_pp, a, bt, M, N, K, lda, ldb, e); break; \
+      case E * 3 + 1: launch_big<E, true, false>(use_pp, a, bt, M, N, K, lda, ldb, e); break;
       LB(EPI_QKV) LB(EPI_RESID) LB(EPI_GELU) LB(EPI_NULL)
 #undef LB
-      case EPI_QKV * 3 + 2: launch_big<EPI_QKV, true, true>(pp, a, bt, M, N, K, lda, ldb, e); break;
-      case EPI_GELU * 3 + 2: launch_big<EPI_GELU, true, true>(pp, a, bt, M, N, K, lda, ldb, e); break;
+      case EPI_QKV * 3 + 2: launch_big<EPI_QKV, true, true>(use_pp, a, bt, M, N, K, lda, ldb, e); break;
+      case EPI_GELU * 3 + 2: launch_big<EPI_GELU, true, true>(use_pp, a, bt, M, N, K, lda, ldb, e); break;
       default: return fail("nqk_qgemm_fused: no big-tile kernel for this epilogue");
     }
     return launch_status("nqk_qgemm_fused(big)");

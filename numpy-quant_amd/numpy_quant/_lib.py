@@ -33,7 +33,7 @@ class Epilogue(ctypes.Structure):
                 ("s_acc", ctypes.c_float * 3), ("s_out", ctypes.c_float * 3), ("zp_out", ctypes.c_int64 * 3),
                 ("out", ctypes.c_void_p * 3), ("bias", ctypes.c_void_p), ("resid", ctypes.c_void_p),
                 ("div", ctypes.c_float), ("add1", ctypes.c_float), ("mul2", ctypes.c_float),
-                ("pad1", ctypes.c_float)]
+                ("b_packed", ctypes.c_int32)]
 
 
 class Attention(ctypes.Structure):
@@ -85,6 +85,7 @@ SIGNATURES = {
     "nqk_minmax_f32": [_p, _l, _p, _p, _l],
     "nqk_copy_strided": [_p, _p, _i, _i, _lp, _lp, _lp],
     "nqk_where_f32": [_p, _p, _p, _p, _i, _lp, _lp, _lp, _lp],
+    "nqk_pack_b": [_p, _p, _l, _l, _l],
     "nqk_qgemm_fused": [_i, _p, _p, _l, _l, _l, _l, _l, _l, _lp, _l, _l, ctypes.POINTER(Epilogue)],
     "nqk_ln_quant": [_p, _p, _p, _p, _l, _l, _f, _f, _l, _i],
     "nqk_softmax_quant": [_p, _p, _p, _l, _l, _l, _f, _l, _i],

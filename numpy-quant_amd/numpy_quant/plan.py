@@ -15,6 +15,7 @@ the layer to the eager loop.
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from typing import Optional
 
@@ -458,6 +459,10 @@ class FusedLayer:
         self.s_wo, self.s_w1, self.s_w2 = m.wo.data.scale, m.w1.data.scale, m.w2.data.scale
         self.bias_o, self.bias_1, self.bias_2 = deq(m.bo).dev, deq(m.b1).dev, deq(m.b2).dev
         self.F = self.bt_1.shape[0]
+        # tile-packed weight images (whole 128-B lines per LDS-DMA piece), when the big-tile
+        # GEMM takes the shape
+        self.bp = {k: _pack_b(b) for k, b in (("qkv", self.bt_qkv), ("o", self.bt_o), ("1", self.bt_1),
+                                               ("2", self.bt_2))}
         # max |column sum| of each weight: lets the GEMM epilogues prove f32 exactness
         self.cmax = {k: _absmax(c) for k, c in (("qkv", self.col_qkv), ("o", self.col_o), ("1", self.col_1),
                                                  ("2", self.col_2))}
@@ -483,6 +488,12 @@ class FusedLayer:
             else:
                 setattr(e, k, v)
         return e
+
+    def _b(self, e, key, bt):
+        """The B operand of a projection GEMM: its packed image if there is one."""
+        bp = self.bp[key]
+        e.b_packed = 0 if bp is None else 1
+        return bt if bp is None else bp
 
     def _attention_unfused(self, w, B, T, Tp, H, Dh, D):
         """Scores GEMM, softmax and PV GEMM as three launches (any T / head size)."""
@@ -526,7 +537,7 @@ class FusedLayer:
                       s_out=[_f32(self.p_head[r].scale) for r in "qkv"],
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
                       out=[w["q"].ptr, w["k"].ptr, w["v"].ptr], bias=self.bias_qkv.ptr)
-        _gemm(EPI_QKV, w["lnq"], self.bt_qkv, 1, Mrows, 3 * D, D, D, D, None, 0, 0, e)
+        _gemm(EPI_QKV, w["lnq"], self._b(e, "qkv", self.bt_qkv), 1, Mrows, 3 * D, D, D, D, None, 0, 0, e)
         pq, pk, pv_ = self.p_head["q"], self.p_head["k"], self.p_head["v"]
         if self.attn_fused:
             # 3-6) one kernel per (image, head): scores, softmax, P V, context quantize
@@ -548,7 +559,7 @@ class FusedLayer:
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr, col_absmax=self.cmax["o"],
                       s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
                       resid=x.dev.ptr, out=[x1.ptr])
-        _gemm(EPI_RESID, w["ctx"], self.bt_o, 1, Mrows, D, D, D, D, None, 0, 0, e)
+        _gemm(EPI_RESID, w["ctx"], self._b(e, "o", self.bt_o), 1, Mrows, D, D, D, D, None, 0, 0, e)
         # 8) LN2 + quantize
         _ln_quant(x1, self.g2, self.be2, w["ln2q"], Mrows, D, self.eps2, self.p_ln2, bw)
         # 9) FFN up + bias + GELU + quantize
@@ -556,14 +567,25 @@ class FusedLayer:
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
                       s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[w["h"].ptr],
                       div=m.gelu_div, add1=m.gelu_add, mul2=m.gelu_mul)
-        _gemm(EPI_GELU, w["ln2q"], self.bt_1, 1, Mrows, F, D, D, D, None, 0, 0, e)
+        _gemm(EPI_GELU, w["ln2q"], self._b(e, "1", self.bt_1), 1, Mrows, F, D, D, D, None, 0, 0, e)
         # 10) FFN down + bias + residual
         x2 = DeviceArray((B, T, D), np.float32)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr, col_absmax=self.cmax["2"],
                       s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
                       resid=x1.ptr, out=[x2.ptr])
-        _gemm(EPI_RESID, w["h"], self.bt_2, 1, Mrows, D, F, F, F, None, 0, 0, e)
+        _gemm(EPI_RESID, w["h"], self._b(e, "2", self.bt_2), 1, Mrows, D, F, F, F, None, 0, 0, e)
         m.x_out.data = FTensor(x2)
+
+
+def _pack_b(bt):
+    """nqk_pack_b image of a constant Bt [N][K] (None where the big-tile GEMM does not take
+    the shape, or NQK_NO_BPACK is set)."""
+    N, K = bt.shape
+    if K % 192 or N % 4 or os.environ.get("NQK_NO_BPACK"):
+        return None
+    out = DeviceArray(((N + 255) // 256 * 256, K), np.int8)
+    _lib.call("nqk_pack_b", bt.vp, out.vp, N, K, K)
+    return out
 
 
 def _absmax(col) -> int:

@@ -90,7 +90,7 @@ def test_patchify_dequant_equals_dequantize_then_im2col(n, c, h, w, kh, kw, zp):
 
 
 _VARIANTS = [{}, {"NQK_GEMM_PP": "1"}, {"NQK_NO_F32X": "1"}, {"NQK_NO_F32X": "1", "NQK_GEMM_PP": "1"},
-             {"NQK_NO_GELU_FILTER": "1", "NQK_NO_F32X": "1"}]
+             {"NQK_NO_GELU_FILTER": "1", "NQK_NO_F32X": "1"}, {"PACK": "1"}, {"PACK": "1", "NQK_NO_F32X": "1"}]
 
 
 @pytest.mark.parametrize("epi_name,M,N,K,zpa,s_out,zp", [
@@ -104,8 +104,9 @@ _VARIANTS = [{}, {"NQK_GEMM_PP": "1"}, {"NQK_NO_F32X": "1"}, {"NQK_NO_F32X": "1"
     ("gelu", 513, 512, 1536, -1, (0.02, 1, 1), (0, 0, 0)),
 ])
 def test_projection_gemm_variants_agree(epi_name, M, N, K, zpa, s_out, zp, monkeypatch):
-    """Projection GEMM variants: the ping-pong 256x256 kernel (k_qgemm_pp) or the 128x256
-    one (k_qgemm_big), f64 or proven-exact f32 epilogue arithmetic with rounding filters,
+    """Projection GEMM variants: the 128x256 kernel (k_qgemm_big) with row-major or
+    tile-packed weights (nqk_pack_b), the ping-pong 256x256 kernel (k_qgemm_pp), f64 or
+    proven-exact f32 epilogue arithmetic with rounding filters,
     GELU filter on or off -- all bit-identical, on ragged tiles and small output scales
     that put many values next to rounding boundaries.  The exact-chain variant is itself
     checked against the reference's node loop by the plan tests."""
@@ -121,12 +122,17 @@ def test_projection_gemm_variants_agree(epi_name, M, N, K, zpa, s_out, zp, monke
     col = DeviceArray.from_host(col_h)
     bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
     resid = DeviceArray.from_host(rng.standard_normal((M, N)).astype(np.float32))
+    from numpy_quant.plan import _pack_b
+    packed = _pack_b(bt)  # None where the big-tile kernel does not take the shape
     outs = []
     for var in _VARIANTS:
+        if "PACK" in var and packed is None:
+            continue
         for k in ("NQK_GEMM_PP", "NQK_NO_F32X", "NQK_NO_GELU_FILTER"):
             monkeypatch.delenv(k, raising=False)
         for k, v in var.items():
-            monkeypatch.setenv(k, v)
+            if k != "PACK":
+                monkeypatch.setenv(k, v)
         e = _lib.Epilogue()
         e.zp_flags, e.bit_width = _lib.ZP_COL, 8
         e.zpa, e.col, e.col_absmax = zpa, col.ptr, int(np.abs(col_h).max())
@@ -147,7 +153,8 @@ def test_projection_gemm_variants_agree(epi_name, M, N, K, zpa, s_out, zp, monke
             bufs = [DeviceArray((M, N), np.int8)]
             e.s_acc[0], e.s_out[0], e.zp_out[0], e.out[0] = float(np.float32(1.3e-4)), s_out[0], zp[0], bufs[0].ptr
             e.div, e.add1, e.mul2 = float(np.float32(1.4142135381698608)), 1.0, 0.5
-        _gemm(epi, a, bt, 1, M, N, K, K, K, None, 0, 0, e)
+        e.b_packed = 1 if "PACK" in var else 0
+        _gemm(epi, a, packed if "PACK" in var else bt, 1, M, N, K, K, K, None, 0, 0, e)
         outs.append([b.to_host() for b in bufs])
     for o in outs[1:]:
         for x, y in zip(outs[0], o):
