@@ -234,7 +234,7 @@ struct EmbedEpi {
   int64_t hw;
 };
 
-template <bool EMBED>
+template <bool EMBED, bool AL16>
 __global__ void __launch_bounds__(256, 2)
 k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
              int64_t N, int64_t K, int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc,
@@ -286,6 +286,38 @@ k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __
     const int cur = (int)(kt & 1);
     if (kt + 1 < nk) load((kt + 1) * 16);
     const int64_t k0 = kt * 16;
+    if constexpr (AL16) {
+      // K and every BLAS block end are multiples of 16: a whole static k-tile, the block
+      // boundary (if any) at its end
+#pragma unroll
+      for (int kk = 0; kk < 16; kk += 2) {
+        float a[2], b[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = sa[cur][kk + h][wm * 64 + i * 32 + r32];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] = sb[cur][kk + h][wn * 64 + j * 32 + r32];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      if (k0 + 16 == bend) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              tot[i][j][r] = tot[i][j][r] + acc[i][j][r];
+              acc[i][j][r] = 0.0f;
+            }
+        ++blk;
+        bend = blk < kb.n ? kb.end[blk] : -1;
+      }
+      if (kt + 1 < nk) store(cur ^ 1);
+      __syncthreads();
+      continue;
+    }
     const int kmax = (int)((K - k0) < 16 ? (K - k0) : 16);  // even
     for (int kk = 0; kk < kmax; kk += 2) {
       float a[2], b[2];
@@ -426,6 +458,16 @@ static int blas_kblocks(int64_t K, KBlocks* kb) {
 
 using namespace nqk;
 
+// K and every BLAS block end multiples of 16 (k_sgemm_mfma AL16; NQK_SGEMM_AL16=0 disables)
+static bool kblocks_al16(int64_t K, const KBlocks& kb) {
+  const char* v = getenv("NQK_SGEMM_AL16");
+  if (v && atoi(v) == 0) return false;
+  if (K % 16) return false;
+  for (int i = 0; i < kb.n; ++i)
+    if (kb.end[i] % 16) return false;
+  return true;
+}
+
 extern "C" int nqk_qgemm_i8(const int8_t* a, const int8_t* bt, int32_t* c, int64_t batch, int64_t M, int64_t N,
                             int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const int64_t* bmap,
                             int64_t a_mat_stride, int64_t b_mat_stride, int64_t c_mat_stride) {
@@ -470,8 +512,12 @@ extern "C" int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch
   if ((K & 1) == 0 && K > 0 && M * N >= 128 * 128 && !getenv("NQK_SGEMM_VALU")) {
     dim3 g2((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128), (unsigned)batch);
     if ((M + 127) / 128 > 65535) return fail("nqk_sgemm: grid too large");
-    hipLaunchKernelGGL(k_sgemm_mfma<false>, g2, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk, b_sk, b_sn, ldc,
-                       m, a_mat_stride, b_mat_stride, c_mat_stride, kb, EmbedEpi{nullptr, nullptr, 1});
+    if (kblocks_al16(K, kb))
+      hipLaunchKernelGGL((k_sgemm_mfma<false, true>), g2, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk, b_sk,
+                         b_sn, ldc, m, a_mat_stride, b_mat_stride, c_mat_stride, kb, EmbedEpi{nullptr, nullptr, 1});
+    else
+      hipLaunchKernelGGL((k_sgemm_mfma<false, false>), g2, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk, b_sk,
+                         b_sn, ldc, m, a_mat_stride, b_mat_stride, c_mat_stride, kb, EmbedEpi{nullptr, nullptr, 1});
     return launch_status("nqk_sgemm(mfma)");
   }
   dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64), (unsigned)batch);
@@ -490,8 +536,12 @@ extern "C" int nqk_sgemm_embed(const float* cols, const float* w, const float* b
   if (blas_kblocks(K, &kb)) return fail("nqk_sgemm_embed: K too large for the BLAS blocking table");
   const BatchMap m = batch_map(nullptr);
   dim3 g2((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128), 1);
-  hipLaunchKernelGGL(k_sgemm_mfma<true>, g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1, N,
-                     (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
+  if (kblocks_al16(K, kb))
+    hipLaunchKernelGGL((k_sgemm_mfma<true, true>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1, N,
+                       (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
+  else
+    hipLaunchKernelGGL((k_sgemm_mfma<true, false>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1,
+                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
   if (int rc = launch_status("nqk_sgemm_embed")) return rc;
   hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);
   return launch_status("nqk_sgemm_embed(cls)");
