@@ -253,7 +253,7 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
   } else {
     uint32_t packed = 0;
     if constexpr (EPI == EPI_GELU) {
-      if (e.gelu_filter) {
+      if (F32X || e.gelu_filter) {  // F32X is only chosen with the filter (host)
         // filter: gelu_fast is within GELU_REL*|h| + GELU_ABS of the exact chain (checked
         // on all 2^32 inputs); h comes from an f32 dequant, which equals the f64 one for
         // |v| < 2^24 (v and s_acc exact in f32, one rounding); t = y / s from an f32
@@ -1181,7 +1181,7 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     const int ng = epi == EPI_QKV ? 3 : 1;
     bool zp_small = true;
     for (int g = 0; g < ng; ++g) zp_small = zp_small && params->zp_out[g] >= -(1 << 20) && params->zp_out[g] <= (1 << 20);
-    const bool f32x = i32 && (epi == EPI_QKV || epi == EPI_GELU) && zp_small &&
+    const bool f32x = i32 && (epi == EPI_QKV || (epi == EPI_GELU && e.gelu_filter)) && zp_small &&
                       16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
     const bool use_pp = pp && !params->b_packed;
     switch (epi * 3 + (f32x ? 2 : (i32 ? 1 : 0))) {

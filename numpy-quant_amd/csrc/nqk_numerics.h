@@ -107,18 +107,19 @@ __device__ __forceinline__ float gelu_ref(float h, double rdiv, float add1, floa
 // |gelu_fast(h) - gelu_ref(h)| <= GELU_REL * |h| + GELU_ABS; the GEMM epilogue only
 // trusts gelu_fast where that bound cannot move the quantized value (nqk_fused.hip).
 constexpr float GELU_REL = 0x1p-20f, GELU_ABS = 0x1p-60f;
+// With A&S 7.1.26 erf(x) = 1 - P(t) t e^{-x^2}, t = 1 / (1 + p|x|), x = h / sqrt2, the
+// GELU h (1 + erf(x)) / 2 is max(h, 0) - |h| q with q = P(t) t e^{-h^2/2} / 2 (the 1/2
+// and 1/sqrt2 folded into the constants): 12 VALU + v_rcp + v_exp.
 __device__ __forceinline__ float gelu_fast(float h) {
-  const float x = h * 0.70710677f;
-  const float ax = __builtin_fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, ax, 1.0f));
-  float p = __builtin_fmaf(1.061405429f, t, -1.453152027f);
-  p = __builtin_fmaf(p, t, 1.421413741f);
-  p = __builtin_fmaf(p, t, -0.284496736f);
-  p = __builtin_fmaf(p, t, 0.254829592f);
-  const float e = __builtin_amdgcn_exp2f(-(ax * ax) * 1.44269504f);
-  const float y = __builtin_fmaf(-(p * t), e, 1.0f);
-  const float erf = __builtin_copysignf(y, x);
-  return (h * (erf + 1.0f)) * 0.5f;
+  const float ah = __builtin_fabsf(h);
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f * 0.70710677f, ah, 1.0f));
+  float p = __builtin_fmaf(0.5f * 1.061405429f, t, 0.5f * -1.453152027f);
+  p = __builtin_fmaf(p, t, 0.5f * 1.421413741f);
+  p = __builtin_fmaf(p, t, 0.5f * -0.284496736f);
+  p = __builtin_fmaf(p, t, 0.5f * 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(h * (h * -0.72134752f));  // e^{-h^2/2}
+  const float q = (p * t) * e;
+  return __builtin_fmaxf(h, 0.0f) - ah * q;
 }
 
 // ------------------------------------------------------------------ NumPy pairwise sum
