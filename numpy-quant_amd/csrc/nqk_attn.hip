@@ -41,7 +41,7 @@ __device__ __forceinline__ int quant_filter(float tf, float zpf, float lof, floa
   const float r = __builtin_rintf(tf);
   const float room = 0.5f - __builtin_fabsf(tf - r);
   *slow = !(room > __builtin_fabsf(tf) * 0x1p-21f + 0x1p-126f);
-  return (int)__builtin_fminf(__builtin_fmaxf(r + zpf, lof), hif);
+  return (int)__builtin_amdgcn_fmed3f(r + zpf, lof, hif);  // r finite here unless *slow
 }
 
 __device__ __forceinline__ int swz64a(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }

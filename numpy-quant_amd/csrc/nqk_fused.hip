@@ -578,6 +578,9 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
 
 // XCD-aware tile order: XCD x (= blockIdx % 8) walks one contiguous band of tiles, so
 // the blocks that share an A row panel share one L2
+#ifndef NQK_LN_DIAG
+#define NQK_LN_DIAG 0
+#endif
 #ifndef NQK_TILE_ORDER
 #define NQK_TILE_ORDER 0  // diagnostic builds: 1 = plain block order, 2 = column-panel bands
 #endif
@@ -925,8 +928,15 @@ k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const f
   const int c0 = leaf * LF + 4 * grp;
   const float* xr = x + (ok ? row : 0) * COLS + c0;
   float4 xv[NI];
+#if NQK_LN_DIAG
+  // diagnostic only (wrong values): fully coalesced loads of the wave's rows
+  const float* wbase = x + (((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63)) / LPR) * COLS;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) xv[i] = *reinterpret_cast<const float4*>(wbase + (i * 64 + lane) * 4);
+#else
 #pragma unroll
   for (int i = 0; i < NI; ++i) xv[i] = *reinterpret_cast<const float4*>(xr + 8 * i);
+#endif
   float a0 = xv[0].x, a1 = xv[0].y, a2 = xv[0].z, a3 = xv[0].w;
 #pragma unroll
   for (int i = 1; i < NI; ++i) {
