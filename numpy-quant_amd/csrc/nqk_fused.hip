@@ -578,6 +578,9 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
 
 // XCD-aware tile order: XCD x (= blockIdx % 8) walks one contiguous band of tiles, so
 // the blocks that share an A row panel share one L2
+#ifndef NQK_STAGGER
+#define NQK_STAGGER 0
+#endif
 #ifndef NQK_LN_DIAG
 #define NQK_LN_DIAG 0
 #endif
@@ -613,6 +616,11 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   constexpr int PW = AP + BP;               // LDS-DMA ops per wave per stage (6)
   constexpr int STAGE = (GBM + GBN) * GBK;  // 24 KiB
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+#if NQK_STAGGER
+  // diagnostic: the second block of each CU in the first dispatch round starts late
+  if (blockIdx.x >= 256 && blockIdx.x < 512)
+    for (int i = 0; i < NQK_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   int tm, tn;
   tile_of(xcd_tile(tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
