@@ -80,6 +80,17 @@ def _is_const(v):
     return v.__class__.__name__ == "Constant"
 
 
+def _const_float(qmodel, v):
+    """The float value of a LayerNorm parameter: a quantized Constant (dequantized as the
+    node loop does), or an Identity of one (the ONNX exporter shares equal tensors that
+    way, e.g. the encoder-layer graph's layernorm_after weights)."""
+    while not _is_const(v):
+        if v.__class__.__name__ != "Variable" or len(v.inputs) != 1 or v.inputs[0].op != "Identity":
+            raise NoMatch(f"{v.name}: constant LayerNorm parameter expected")
+        v = v.inputs[0].inputs[0]
+    return qmodel._dequant_input(v)
+
+
 def _matmul_weight(node):
     a, w = node.inputs
     if not _is_const(w) or _is_const(a):
@@ -431,8 +442,9 @@ class FusedLayer:
         self.bw = qmodel.bit_width
         qp = qmodel.quant_params
         deq = qmodel._dequant_input
-        self.g1, self.be1 = deq(m.ln1.inputs[1]).dev, deq(m.ln1.inputs[2]).dev
-        self.g2, self.be2 = deq(m.ln2.inputs[1]).dev, deq(m.ln2.inputs[2]).dev
+        cf = lambda v: _const_float(qmodel, v)  # noqa: E731
+        self.g1, self.be1 = cf(m.ln1.inputs[1]).dev, cf(m.ln1.inputs[2]).dev
+        self.g2, self.be2 = cf(m.ln2.inputs[1]).dev, cf(m.ln2.inputs[2]).dev
         self.eps1 = _f32(m.ln1.attrs.get("epsilon", 1e-5))
         self.eps2 = _f32(m.ln2.attrs.get("epsilon", 1e-5))
         self.p_ln1, self.p_ln2 = qp[m.ln1_out.name], qp[m.ln2_out.name]
@@ -517,8 +529,10 @@ class FusedLayer:
     def run(self, ws: "Workspace"):
         m, bw = self.m, self.bw
         x = m.x_in.data
+        if isinstance(x, QTensor):  # a quantized graph input: its LN and residual-Add
+            x = x.dequantize()      # consumers both see the dequantized tensor (model.py:528-538)
         if not isinstance(x, FTensor):
-            raise ValueError("fused layer input must be a float tensor")
+            raise ValueError("fused layer input must be a float or quantized tensor")
         B, T, D = x.dev.shape
         if T != m.tokens or D != self.D:
             raise ValueError(f"layer input {x.dev.shape} does not match the graph ({m.tokens}, {self.D})")

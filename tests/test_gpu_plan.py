@@ -55,3 +55,23 @@ def test_plan_equals_eager(batch, bw):
         layer_outs[layer.m.x_out.name] = None
     fused = qmodel([x])[0]
     np.testing.assert_array_equal(fused, eager)
+
+
+def test_plan_encoder_layer_graph_matches_oracle():
+    """The encoder-layer graph: a quantized graph input feeds the fused layer, and the
+    second LayerNorm's parameters come through Identity nodes (shared by the exporter)."""
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model, QuantizationParams
+    from oracle import nq_oracle as O
+    path = os.path.join(MODELS, "vit_image_classifier_encoder_layer_no_weights.onnx")
+    x = np.random.default_rng(5).standard_normal((1, 197, 768)).astype(np.float32)
+    graph = O.Graph(onnx_proto.load(path, synthetic_weights=True))
+    with np.errstate(all="ignore"):
+        qp, qc = O.calibrate(graph, [x], 8)
+        ref = O.outputs_of(graph, O.quantized_forward(graph, qp, qc, [x], 8))[0]
+    model = Model.from_onnx(onnx_proto.load(path, synthetic_weights=True))
+    qmodel = model.quantize_with({k: QuantizationParams(v.scale, v.zero_point) for k, v in qp.items()}, bit_width=8)
+    np.testing.assert_array_equal(qmodel([x])[0], ref)
+    plan = qmodel.compile()
+    assert plan.fused == 1
+    np.testing.assert_array_equal(qmodel([x])[0], ref)
