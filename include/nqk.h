@@ -201,7 +201,7 @@ typedef struct nqk_epilogue {
   const float* bias;                    /* dequantized bias [N] (EPI_QKV/RESID/GELU)    */
   const float* resid;                   /* residual [M][N] (EPI_RESID)                  */
   float div, add1, mul2;                /* Div constant (8 / sqrt 2), GELU +1 and *0.5  */
-  int32_t b_packed;                     /* bt is the nqk_pack_b image of the weight      */
+  int32_t b_packed;                     /* 1: bt is an nqk_pack_b image; 2: nqk_pack_b4  */
 } nqk_epilogue;
 /* int8 MFMA GEMM C = A . Bt^T (layouts as nqk_qgemm_i8) with a fused epilogue:
  *   QKV    model.py MatMul -> Add(bias) -> Reshape -> Transpose -> quantize, 3 groups
@@ -215,6 +215,10 @@ typedef struct nqk_epilogue {
  * operand is read as whole 128-byte lines (replaces no reference function: a layout of
  * the same numpy_quantization.py:44-61 q_matmul operand). */
 int nqk_pack_b(const int8_t* bt, int8_t* out, int64_t N, int64_t K, int64_t ldb);
+/* int4 weights (every value in [-8, 7], bit width <= 4): the same tiles nibble-packed,
+ * ceil(N/256)*256*K/2 bytes; the GEMM unpacks them in registers after the LDS stage
+ * (b_packed = 2).  BASELINE configs[4] ("int4 packed weights"). */
+int nqk_pack_b4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t ldb);
 int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, int64_t M, int64_t N, int64_t K,
                     int64_t lda, int64_t ldb, const int64_t* bmap, int64_t a_mat_stride, int64_t b_mat_stride,
                     const nqk_epilogue* params);

@@ -519,7 +519,7 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((c
 // loop): each wave owns a G_RP x 72-int32 slice; 128 / G_RP passes of G_RP rows.  Read
 // back row-major, a lane takes 4 consecutive columns of one row, so bias / column terms
 // are per lane and the outputs leave as 4-byte (int8) or 16-byte (f32) stores.
-template <int EPI, bool I32, bool F32X>
+template <int EPI, bool I32, bool F32X, int ASH = 0>
 __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], const Epi& e, int mw, int ncol0,
                                               int M, int N, int wave, int lane) {
   constexpr int RP = G_RP;
@@ -546,7 +546,7 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          stg[(ii * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 72 + j * 32 + r32] = acc[pass * (RP / 32) + ii][j][r];
+          stg[(ii * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 72 + j * 32 + r32] = acc[pass * (RP / 32) + ii][j][r] >> ASH;
     wave_lds_sync();
     // image / token of this lane's row, advanced incrementally (4 rows per step)
     int gm = mw + pass * RP + (lane >> 4);
@@ -606,15 +606,22 @@ __device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& t
   }
 }
 
-template <int EPI, bool I32, bool F32X>
+// B4: the weights are int4 (|w| <= 8), nibble-packed by nqk_pack_b4: a B row of one
+// k-step is 32 bytes, so a stage moves half the B bytes.  A lane's 16 k-values of one
+// MFMA operand are 8 packed bytes (ds_read_b64) that unpack with two AND masks into
+// bytes 16 * w (the nibble lands in the high half, its sign bit on the byte's): the
+// MFMA then accumulates 16 * acc exactly (|acc| <= 2^11 K), and the epilogue takes
+// acc >> 4.
+template <int EPI, bool I32, bool F32X, bool B4 = false>
 __global__ void __launch_bounds__(256, 2)
 k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
             int tiles_m, int tiles_n, Epi e) {
   constexpr int GBM = 128;
-  constexpr int AP = GBM * GBK / 1024 / 4;  // A pieces per wave per stage (2)
-  constexpr int BP = GBN * GBK / 1024 / 4;  // B pieces per wave per stage (4)
-  constexpr int PW = AP + BP;               // LDS-DMA ops per wave per stage (6)
-  constexpr int STAGE = (GBM + GBN) * GBK;  // 24 KiB
+  constexpr int BROW = B4 ? GBK / 2 : GBK;     // bytes of one B row per k-step
+  constexpr int AP = GBM * GBK / 1024 / 4;     // A pieces per wave per stage (2)
+  constexpr int BP = GBN * BROW / 1024 / 4;    // B pieces per wave per stage (4 / 2)
+  constexpr int PW = AP + BP;                  // LDS-DMA ops per wave per stage (6 / 4)
+  constexpr int STAGE = GBM * GBK + GBN * BROW;  // 24 / 16 KiB
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
 #if NQK_STAGGER
   // diagnostic: the second block of each CU in the first dispatch round starts late
@@ -639,12 +646,12 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   }
   // B: row-major Bt, or the tile-packed image of nqk_pack_b (every LDS-DMA piece one
   // contiguous KiB = eight full 128-B lines, the swizzle already applied)
-  const bool bpk = e.b_packed != 0;
-  const int64_t bstep = bpk ? (int64_t)GBN * GBK : GBK;
+  const bool bpk = B4 || e.b_packed != 0;
+  const int64_t bstep = bpk ? (int64_t)GBN * BROW : GBK;
 #pragma unroll
   for (int p = 0; p < BP; ++p) {
     const int row = (wave * BP + p) * 16 + prow;
-    bsrc[p] = bpk ? Bt + (int64_t)tn * (K / GBK) * (GBN * GBK) + (wave * BP + p) * 1024 + lane * 16
+    bsrc[p] = bpk ? Bt + (int64_t)tn * (K / GBK) * (GBN * BROW) + (wave * BP + p) * 1024 + lane * 16
                   : Bt + (int64_t)min(n0 + row, N - 1) * ldb + (ppos ^ ((row >> 2) & 3)) * 16;
   }
   auto issue = [&](int st, auto SLOT) {
@@ -696,8 +703,17 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[s][i] = *reinterpret_cast<const v4i*>(sa + swz64(i * 32 + r32, 2 * half + s));
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[s][j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * half + s));
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (B4) {
+          // row of 4 x 8-byte chunks, chunk c at c ^ ((row >> 3) & 3): conflict-free b64 reads
+          const int row = wn * 64 + j * 32 + r32, c = 2 * half + s;
+          const uint2 w = *reinterpret_cast<const uint2*>(sb + row * 32 + ((c ^ ((row >> 3) & 3)) << 3));
+          fb[s][j] = v4i{(int)((w.x << 4) & 0xF0F0F0F0u), (int)(w.x & 0xF0F0F0F0u), (int)((w.y << 4) & 0xF0F0F0F0u),
+                         (int)(w.y & 0xF0F0F0F0u)};
+        } else {
+          fb[s][j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * half + s));
+        }
+      }
     }
     if constexpr (decltype(refill)::value) issue(kt + 2, std::integral_constant<int, (sl + 2) % GST>{});
 #pragma unroll
@@ -727,6 +743,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
       }
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 10 - (decltype(refill)::value ? PW : 0), 0);
+    static_assert(PW <= 10, "LDS-DMA ops per stage must fit between the MFMAs");
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
@@ -746,7 +763,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   kstep(nk - 1, S2{}, F_{}, T_{});
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  proj_epilogue<EPI, I32, F32X>(lds, acc, e, m0, n0 + wn * 64, M, N, wave, lane);
+  proj_epilogue<EPI, I32, F32X, B4 ? 4 : 0>(lds, acc, e, m0, n0 + wn * 64, M, N, wave, lane);
 }
 
 template <int EPI, bool I32, bool F32X>
@@ -877,6 +894,29 @@ __global__ void k_pack_b(const int8_t* __restrict__ bt, int8_t* __restrict__ out
     v4i v = {0, 0, 0, 0};
     if (n < N) v = *reinterpret_cast<const v4i*>(bt + n * ldb + kt * GBK + ((pos ^ ((row >> 2) & 3)) << 4));
     *reinterpret_cast<v4i*>(out + c * 16) = v;
+  }
+}
+
+// nibble-packed int4 image of a weight Bt [N][K] with every value in [-8, 7], for
+// k_qgemm_big<B4>: per column panel tn and k-step kt a 256 x 32-byte block; row chunk c
+// (k = 16c .. 16c + 15) at chunk position c ^ ((row >> 3) & 3); inside a chunk byte b of
+// word h (h = 0, 1) holds k = 16c + 8h + b in its low nibble and k = 16c + 8h + 4 + b in
+// its high nibble (the order the unpack masks of the kernel produce).
+__global__ void k_pack_b4(const int8_t* __restrict__ bt, uint8_t* __restrict__ out, int64_t N, int64_t K,
+                          int64_t ldb, int64_t total) {
+  const int64_t nk = K / GBK;
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t blk = o >> 13, w = o & 8191;  // 8 KiB per block
+    const int64_t tn = blk / nk, kt = blk - tn * nk;
+    const int row = (int)(w >> 5), pos = (int)((w >> 3) & 3), bb = (int)(w & 7);
+    const int c = pos ^ ((row >> 3) & 3), h = bb >> 2, b = bb & 3;
+    const int64_t n = tn * GBN + row;
+    uint8_t v = 0;
+    if (n < N) {
+      const int8_t* src = bt + n * ldb + kt * GBK + 16 * c + 8 * h;
+      v = (uint8_t)((src[b] & 0xF) | ((src[4 + b] & 0xF) << 4));
+    }
+    out[o] = v;
   }
 }
 
@@ -1088,6 +1128,14 @@ template <int EPI, bool I32, bool F32X>
 static void launch_big(bool pp, const int8_t* a, const int8_t* bt, int64_t M, int64_t N, int64_t K, int64_t lda,
                        int64_t ldb, const Epi& e) {
   const int tn = (int)((N + GBN - 1) / GBN);
+  if constexpr (I32 && EPI != EPI_NULL) {
+    if (e.b_packed == 2) {  // int4 nibble image (nqk_pack_b4)
+      const int tm = (int)((M + 127) / 128);
+      hipLaunchKernelGGL((k_qgemm_big<EPI, I32, F32X, true>), dim3(tm * tn), dim3(256), BIG_LDS, stream(), a, bt,
+                         (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e);
+      return;
+    }
+  }
   if (pp) {
     const int tm = (int)((M + 255) / 256);
     hipLaunchKernelGGL((k_qgemm_pp<EPI, I32, F32X>), dim3(tm * tn), dim3(512), PP_LDS, stream(), a, bt, (int)M,
@@ -1157,6 +1205,14 @@ extern "C" int nqk_pack_b(const int8_t* bt, int8_t* out, int64_t N, int64_t K, i
   return launch_status("nqk_pack_b");
 }
 
+extern "C" int nqk_pack_b4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t ldb) {
+  if (N <= 0 || K <= 0) return 0;
+  if (K % GBK) return fail("nqk_pack_b4: K must be a multiple of 64");
+  const int64_t total = pack_b_bytes(N, K) / 2;
+  hipLaunchKernelGGL(k_pack_b4, dim3(grid_for(total)), dim3(kThreads), 0, stream(), bt, out, N, K, ldb, total);
+  return launch_status("nqk_pack_b4");
+}
+
 extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, int64_t M, int64_t N,
                                int64_t K, int64_t lda, int64_t ldb, const int64_t* bmap, int64_t a_mat_stride,
                                int64_t b_mat_stride, const nqk_epilogue* params) {
@@ -1189,6 +1245,8 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   bool scales_ok = normal(params->s_out[0]) || epi == EPI_RESID || epi == EPI_NULL;
   if (epi == EPI_QKV) scales_ok = normal(params->s_out[0]) && normal(params->s_out[1]) && normal(params->s_out[2]);
   if (epi == EPI_GELU) scales_ok = scales_ok && normal(params->div);
+  if (params->b_packed == 2 && (!i32 || epi == EPI_NULL))
+    return fail("nqk_qgemm_fused: int4 packed weights need the int32 zero-point algebra");
   if (params->b_packed && !(big && aligned && scales_ok && (K % (GST * GBK)) == 0))
     return fail("nqk_qgemm_fused: a packed B operand needs the big-tile path (K % 192 == 0, N % 4 == 0, "
                 "COL zero-point term, aligned outputs)");

@@ -86,6 +86,7 @@ SIGNATURES = {
     "nqk_copy_strided": [_p, _p, _i, _i, _lp, _lp, _lp],
     "nqk_where_f32": [_p, _p, _p, _p, _i, _lp, _lp, _lp, _lp],
     "nqk_pack_b": [_p, _p, _l, _l, _l],
+    "nqk_pack_b4": [_p, _p, _l, _l, _l],
     "nqk_qgemm_fused": [_i, _p, _p, _l, _l, _l, _l, _l, _l, _lp, _l, _l, ctypes.POINTER(Epilogue)],
     "nqk_ln_quant": [_p, _p, _p, _p, _l, _l, _f, _f, _l, _i],
     "nqk_softmax_quant": [_p, _p, _p, _l, _l, _l, _f, _l, _i],

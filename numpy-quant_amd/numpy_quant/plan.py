@@ -473,8 +473,8 @@ class FusedLayer:
         self.F = self.bt_1.shape[0]
         # tile-packed weight images (whole 128-B lines per LDS-DMA piece), when the big-tile
         # GEMM takes the shape
-        self.bp = {k: _pack_b(b) for k, b in (("qkv", self.bt_qkv), ("o", self.bt_o), ("1", self.bt_1),
-                                               ("2", self.bt_2))}
+        self.bp = {k: _pack_b(b, self.bw) for k, b in (("qkv", self.bt_qkv), ("o", self.bt_o), ("1", self.bt_1),
+                                                        ("2", self.bt_2))}
         # max |column sum| of each weight: lets the GEMM epilogues prove f32 exactness
         self.cmax = {k: _absmax(c) for k, c in (("qkv", self.col_qkv), ("o", self.col_o), ("1", self.col_1),
                                                  ("2", self.col_2))}
@@ -504,8 +504,8 @@ class FusedLayer:
     def _b(self, e, key, bt):
         """The B operand of a projection GEMM: its packed image if there is one."""
         bp = self.bp[key]
-        e.b_packed = 0 if bp is None else 1
-        return bt if bp is None else bp
+        e.b_packed = 0 if bp is None else bp[1]
+        return bt if bp is None else bp[0]
 
     def _attention_unfused(self, w, B, T, Tp, H, Dh, D):
         """Scores GEMM, softmax and PV GEMM as three launches (any T / head size)."""
@@ -591,15 +591,21 @@ class FusedLayer:
         m.x_out.data = FTensor(x2)
 
 
-def _pack_b(bt):
-    """nqk_pack_b image of a constant Bt [N][K] (None where the big-tile GEMM does not take
-    the shape, or NQK_NO_BPACK is set)."""
+def _pack_b(bt, bit_width=8):
+    """(image, kind) of a constant Bt [N][K] for the big-tile GEMM: kind 1 = nqk_pack_b
+    (int8 tiles), kind 2 = nqk_pack_b4 (nibble-packed int4, bit widths <= 4, whose
+    symmetric weights lie in [-8, 7]; NQK_NO_B4 disables); None where the big-tile GEMM
+    does not take the shape, or NQK_NO_BPACK is set."""
     N, K = bt.shape
     if K % 192 or N % 4 or os.environ.get("NQK_NO_BPACK"):
         return None
+    if bit_width <= 4 and not os.environ.get("NQK_NO_B4"):
+        out = DeviceArray(((N + 255) // 256 * 256, K // 2), np.uint8)
+        _lib.call("nqk_pack_b4", bt.vp, out.vp, N, K, K)
+        return out, 2
     out = DeviceArray(((N + 255) // 256 * 256, K), np.int8)
     _lib.call("nqk_pack_b", bt.vp, out.vp, N, K, K)
-    return out
+    return out, 1
 
 
 def _absmax(col) -> int:
@@ -631,7 +637,9 @@ def _gemm(epi, a, bt, batch, M, N, K, lda, ldb, bmap, a_ms, b_ms, e):
         raise ValueError("fused GEMM operands must be 16-byte padded")
     need_a = (batch - 1) * a_ms + (M - 1) * lda + K if batch > 1 else (M - 1) * lda + K
     need_b = (batch - 1) * b_ms + (N - 1) * ldb + K if batch > 1 else (N - 1) * ldb + K
-    if need_a > a.size or need_b > bt.size:
+    if e.b_packed:  # a tile-packed image: nqk_pack_b / nqk_pack_b4 sized it for (N, K)
+        need_b = ((N + 255) // 256 * 256) * K // (2 if e.b_packed == 2 else 1)
+    if need_a > a.size or need_b > bt.size * bt.dtype.itemsize:
         raise ValueError("fused GEMM operand smaller than its shape")
     t0 = KM.TIMER.begin() if KM.TIMER is not None else None
     _lib.call("nqk_qgemm_fused", epi, a.vp, bt.vp, batch, M, N, K, lda, ldb,

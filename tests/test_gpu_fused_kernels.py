@@ -123,7 +123,8 @@ def test_projection_gemm_variants_agree(epi_name, M, N, K, zpa, s_out, zp, monke
     bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
     resid = DeviceArray.from_host(rng.standard_normal((M, N)).astype(np.float32))
     from numpy_quant.plan import _pack_b
-    packed = _pack_b(bt)  # None where the big-tile kernel does not take the shape
+    packed = _pack_b(bt)  # (image, 1), or None where the big-tile kernel does not take the shape
+    packed = None if packed is None else packed[0]
     outs = []
     for var in _VARIANTS:
         if "PACK" in var and packed is None:
@@ -159,3 +160,49 @@ def test_projection_gemm_variants_agree(epi_name, M, N, K, zpa, s_out, zp, monke
     for o in outs[1:]:
         for x, y in zip(outs[0], o):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("epi_name,M,N,K", [("qkv", 3 * 197, 2304, 768), ("resid", 1000, 768, 3072),
+                                           ("gelu", 1024 + 77, 3072, 768), ("resid", 77, 772, 192)])
+def test_int4_packed_weights_equal_int8_path(epi_name, M, N, K, monkeypatch):
+    """BASELINE configs[4]: bit width 4, weights nibble-packed (nqk_pack_b4) and unpacked
+    in registers after the LDS stage; the outputs equal the int8-stored path bit for bit."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_GELU, EPI_QKV, EPI_RESID, _gemm, _pack_b
+    epi = {"qkv": EPI_QKV, "resid": EPI_RESID, "gelu": EPI_GELU}[epi_name]
+    rng = np.random.default_rng(M + N + K + 4)
+    a = DeviceArray.from_host(rng.integers(-8, 8, size=(M, K), dtype=np.int8))
+    bt_h = rng.integers(-8, 8, size=(N, K), dtype=np.int8)
+    bt = DeviceArray.from_host(bt_h)
+    col_h = bt_h.astype(np.int64).sum(axis=1)
+    col = DeviceArray.from_host(col_h)
+    bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
+    resid = DeviceArray.from_host(rng.standard_normal((M, N)).astype(np.float32))
+    p4, kind = _pack_b(bt, 4)
+    assert kind == 2
+    outs = []
+    for b_op, kind in ((bt, 0), (p4, 2)):
+        e = _lib.Epilogue()
+        e.zp_flags, e.bit_width, e.zpa, e.col, e.col_absmax = _lib.ZP_COL, 4, 3, col.ptr, int(np.abs(col_h).max())
+        e.bias, e.b_packed = bias.ptr, kind
+        if epi == EPI_QKV:
+            T, H, Dh = 197, N // 3 // 64, 64
+            e.group_cols, e.tokens, e.heads, e.hdim = N // 3, T, H, Dh
+            bufs = [DeviceArray((M // T * H * T, Dh), np.int8) for _ in range(3)]
+            for g in range(3):
+                e.s_acc[g] = float(np.float32(3e-3 * (g + 1)))
+                e.s_out[g], e.zp_out[g], e.out[g] = 0.07 * (g + 1), g - 1, bufs[g].ptr
+        elif epi == EPI_RESID:
+            e.group_cols = 1 << 30
+            bufs = [DeviceArray((M, N), np.float32)]
+            e.s_acc[0], e.out[0], e.resid = float(np.float32(3.1e-3)), bufs[0].ptr, resid.ptr
+        else:
+            e.group_cols = 1 << 30
+            bufs = [DeviceArray((M, N), np.int8)]
+            e.s_acc[0], e.s_out[0], e.zp_out[0], e.out[0] = float(np.float32(2e-3)), 0.11, -2, bufs[0].ptr
+            e.div, e.add1, e.mul2 = float(np.float32(1.4142135381698608)), 1.0, 0.5
+        _gemm(epi, a, b_op, 1, M, N, K, K, K, None, 0, 0, e)
+        outs.append([b.to_host() for b in bufs])
+    for x, y in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(x, y)
