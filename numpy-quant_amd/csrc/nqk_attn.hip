@@ -32,6 +32,7 @@ struct AttnArgs {
   float s_qk, div, s_p, s_pv, s_ctx;
   double rdiv, rs_p, zp_p, rs_ctx, zp_ctx, lo, hi;
   float inv_div, rs_ctx_f, zp_p_f, zp_ctx_f, lo_f, hi_f;  // FAST path constants
+  float s_qkd;  // s_qk / div (div a power of two, s_qk / div in [2^-100, 2^100]: exact)
 };
 
 // rint(zp + t) for t approximated by tf with |t - tf| <= |tf| * 2^-21: decided by tf when
@@ -180,7 +181,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           const int r = 4 * qq + j, n = c * 32 + 8 * qq + 4 * h + j;
           const int vv = acc[c][r] - rowterm - ck[j];
           float y;
-          if constexpr (FAST) y = ((float)vv * a.s_qk) * a.inv_div;
+          // FAST: RN(v s) / 2^k == RN(v (s / 2^k)) while both are normal (host-checked)
+          if constexpr (FAST) y = (float)vv * a.s_qkd;
           else y = div_rc_w((float)((double)vv * (double)a.s_qk), a.rdiv);
           // -inf for padded columns: an add of a selected constant, so no branch
           y = y + (n < T ? 0.0f : -__builtin_inff());
@@ -394,6 +396,7 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   a.lo = -__builtin_ldexp(1.0, p->bit_width - 1);
   a.hi = __builtin_ldexp(1.0, p->bit_width - 1) - 1.0;
   a.inv_div = 1.0f / p->div;
+  a.s_qkd = p->s_qk * a.inv_div;
   a.rs_ctx_f = (float)a.rs_ctx;
   a.zp_p_f = (float)p->zp_p;
   a.zp_ctx_f = (float)p->zp_ctx;
@@ -407,6 +410,7 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   int dexp = 0;
   const float dm = frexpf(p->div, &dexp);
   const bool fast = bs < 16777216.0 && bp < 16777216.0 && dm == 0.5f && llabs(p->zp_ctx) < (1 << 20) &&
+                    normal(a.s_qkd) && normal(p->s_qk) &&
                     !getenv("NQK_ATTN_EXACT");
   const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + (size_t)(NT * 32 + 64) * 4;
   const dim3 grid((unsigned)batch_heads);

@@ -963,8 +963,11 @@ k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float
 // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) combine and the leaf tree are xor-butterflies
 // (float addition is commutative, only the grouping matters).  2*NL lanes per row,
 // 64 / (2*NL) rows per wave; every load and store is 16 / 4 bytes per lane.
+#ifndef NQK_LN_LB
+#define NQK_LN_LB 1
+#endif
 template <int NL>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, NQK_LN_LB)
 k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
                int8_t* __restrict__ out, int64_t rows, float eps, float s, double rs, double zp, double lo,
                double hi) {
