@@ -502,12 +502,18 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
 constexpr int GBN = 256, GBK = 64, GST = 3;
 constexpr int G_RP = 32;                          // epilogue rows per pass and wave
 constexpr int BIG_LDS = GST * (128 + GBN) * GBK;  // 72 KiB (>= 4 waves' staging, 36 KiB)
-constexpr int PP_LDS = GST * (256 + GBN) * GBK;   // 96 KiB (>= 8 waves' staging, 72 KiB)
+#ifndef NQK_PP_PD
+#define NQK_PP_PD 2  // ping-pong ring: stages in flight ahead of the one being read
+#endif
+constexpr int PP_LDS = (NQK_PP_PD + 1) * (256 + GBN) * GBK;  // 96 KiB at depth 2 (>= 72 KiB staging)
 // Diagnostic builds only (tools/gemm_diag.sh, never the shipped library): bit 1 = no
 // global loads in the k loop, 2 = no LDS fragment reads, 4 = no k-step barrier, 8 = no MFMA
 // (k_qgemm_big).
 #ifndef NQK_DIAG
 #define NQK_DIAG 0
+#endif
+#ifndef NQK_GLDS_FIRST
+#define NQK_GLDS_FIRST 0  // diagnostic builds: issue the next stage's LDS-DMA before the reads
 #endif
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -690,6 +696,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     __builtin_amdgcn_sched_barrier(0);
     const int8_t* sa = lds + sl * STAGE;
     const int8_t* sb = sa + GBM * GBK;
+    if constexpr (NQK_GLDS_FIRST && decltype(refill)::value) issue(kt + 2, std::integral_constant<int, (sl + 2) % GST>{});
     v4i fa[2][4], fb[2][2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -715,7 +722,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
         }
       }
     }
-    if constexpr (decltype(refill)::value) issue(kt + 2, std::integral_constant<int, (sl + 2) % GST>{});
+    if constexpr (!NQK_GLDS_FIRST && decltype(refill)::value) issue(kt + 2, std::integral_constant<int, (sl + 2) % GST>{});
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -729,6 +736,17 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
         }
     // issue order: the s=0 fragment reads, then the MFMAs with the s=1 reads and the
     // next stage's loads spread between them
+#if NQK_GLDS_FIRST
+    if constexpr (decltype(refill)::value) __builtin_amdgcn_sched_group_barrier(0x020, PW, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);
+    return;
+#endif
     __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
     for (int g = 0; g < 6; ++g) {
@@ -828,7 +846,7 @@ k_qgemm_pp(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, i
       for (int j = 0; j < 2; ++j)
         fb[s][j] = *reinterpret_cast<const v4i*>(sb + swz64(wn * 64 + j * 32 + r32, 2 * half + s));
     }
-    if (st + 2 < nk) issue(st + 2, slot == 0 ? 2 : slot - 1);
+    if (st + NQK_PP_PD < nk) issue(st + NQK_PP_PD, slot == 0 ? NQK_PP_PD : slot - 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
   // compute segment: 16 MFMAs on the fragments of the last load segment; s_setprio keeps
@@ -853,12 +871,15 @@ k_qgemm_pp(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, i
   };
   // stage st+1 complete for this wave: after each segment, the wave's own pieces of the
   // stage after the one it reads next have landed (at most stage st+2's 4 in flight)
-  auto wait_next = [&](int st) {
-    if (st + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  auto wait_next = [&](int st) {  // allow this wave's pieces of stages st+2 .. st+PD
+    const int n = min(st + NQK_PP_PD, nk - 1) - (st + 1);
+    if (n >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
   issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  for (int st = 1; st < NQK_PP_PD && st < nk; ++st) issue(st, st);
   wait_next(-1);
   barrier();
   // the stagger: group 1 runs one half-step behind group 0, so in every barrier interval
@@ -872,7 +893,7 @@ k_qgemm_pp(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, i
     compute_seg();
     wait_next(st);
     barrier();
-    slot = slot == 2 ? 0 : slot + 1;
+    slot = slot == NQK_PP_PD ? 0 : slot + 1;
   }
   if (grp == 0) barrier();  // same barrier count for both groups
   // every load segment ended (lgkmcnt(0)) before the last barrier: the ring is free
