@@ -19,6 +19,10 @@
 #include "nqk_common.h"
 #include "nqk_numerics.h"
 
+#ifndef NQK_ATTN_DIAG
+#define NQK_ATTN_DIAG 0
+#endif
+
 namespace nqk {
 namespace {
 
@@ -115,10 +119,14 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     const v4i kv = row < T ? *reinterpret_cast<const v4i*>(k + row * 64 + ch * 16) : z;
     const v4i vv = row < T ? *reinterpret_cast<const v4i*>(v + row * 64 + ch * 16) : z;
     *reinterpret_cast<v4i*>(Ks + swz64a(row, ch)) = kv;
+#if NQK_ATTN_DIAG  // diagnostic builds only: V^T staging skipped (wrong context)
+    if (row == 0) Vt[ch] = (int8_t)vv[0];
+#else
 #pragma unroll
     for (int w = 0; w < 4; ++w)
 #pragma unroll
       for (int b = 0; b < 4; ++b) Vt[(ch * 16 + w * 4 + b) * PST + row] = (int8_t)(vv[w] >> (8 * b));
+#endif
   }
   __syncthreads();
   for (int row = tid; row < TP; row += 256) {

@@ -57,6 +57,25 @@ def test_mlp_all_bit_widths():
                     np.testing.assert_array_equal(arr, g[key], err_msg=name)
 
 
+@pytest.mark.parametrize("bw", [8, 4])
+def test_mlp_batch_4096_matches_oracle(bw):
+    """BASELINE configs[1]: mlp.onnx at batch 4096, inputs U[-1.2, 1.2]
+    (seed 4096), calibrated on the committed make_circles X; the device QModel equals the
+    oracle's quantized forward bit for bit (the oracle is pinned to the reference's
+    vectors by test_oracle.py)."""
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model
+    from oracle import nq_oracle as O
+    X = np.load(os.path.join(GOLDEN, "mlp.npz"))["X"]
+    x = np.random.default_rng(4096).uniform(-1.2, 1.2, size=(4096, 2)).astype(np.float32)
+    path = os.path.join(MODELS, "mlp.onnx")
+    graph = O.Graph(onnx_proto.load(path))
+    qp, qc = O.calibrate(graph, [X], bw)
+    ref = O.outputs_of(graph, O.quantized_forward(graph, qp, qc, [x], bw))[0]
+    qmodel = Model.from_onnx(path).quantize([X], bit_width=bw)
+    np.testing.assert_array_equal(qmodel([x])[0], ref)
+
+
 def ref_qparams(meta_qp):
     """QuantizationParams objects equal (values and types) to the reference's."""
     from numpy_quant.model import QuantizationParams

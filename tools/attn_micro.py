@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.join(ROOT, "numpy-quant_amd"))
 from numpy_quant import _lib  # noqa: E402
 from numpy_quant.device import DeviceArray  # noqa: E402
 
+if os.environ.get("GM_LIB"):  # a diagnostic build (tools/gemm_diag.sh)
+    _lib.LIB_PATH = os.environ["GM_LIB"]
 _lib.ensure_init()
 B, H, T, Dh = int(os.environ.get("AM_B", 256)), 12, 197, 64
 rng = np.random.default_rng(0)
