@@ -91,8 +91,14 @@ def kernel_breakdown(qmodel, x_dev):
     achieved rate (int8 ops for MFMA kernels, algorithmic bytes for HBM-bound ones)."""
     from numpy_quant import kernels as K
     K.TIMER = K.KernelTimer()
+    plan = getattr(qmodel, "_plan", None)
+    split = getattr(plan, "split", False)
+    if plan is not None:
+        plan.split = False  # one stream: each launch timed alone
     qmodel.set_inputs([x_dev])
     qmodel.run()
+    if plan is not None:
+        plan.split = split
     recs = K.TIMER.collect()
     K.TIMER = None
     by = {}

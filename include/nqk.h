@@ -62,6 +62,13 @@ int nqk_memcpy_d2d(void* dst, const void* src, size_t bytes);   /* async */
 int nqk_memset(void* ptr, int value, size_t bytes);             /* async */
 int nqk_sync(void);
 int nqk_stream(void** stream);         /* the library's hipStream_t */
+/* a second stream for independent work (the fused plan's two half batches):
+ * nqk_set_stream(1) routes every later call to it, nqk_set_stream(0) back;
+ * nqk_stream_fork makes stream 1 wait for all work issued so far on stream 0,
+ * nqk_stream_join makes stream 0 wait for all work issued so far on stream 1. */
+int nqk_set_stream(int which);
+int nqk_stream_fork(void);
+int nqk_stream_join(void);
 /* stream timers: record start / stop events, nqk_timer_ms waits for stop */
 int nqk_timer_start(void);
 int nqk_timer_stop(void);

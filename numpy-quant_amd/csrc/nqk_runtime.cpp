@@ -9,6 +9,9 @@ namespace {
 thread_local std::string g_err;
 int g_device = -1;
 hipStream_t g_streams[64] = {};
+hipStream_t g_side[64] = {};   // the second stream (nqk_set_stream(1))
+int g_cur = 0;                 // current stream index of the (single) host thread
+hipEvent_t g_fork = nullptr, g_join = nullptr;
 hipEvent_t g_t0 = nullptr, g_t1 = nullptr;
 hipGraph_t g_capturing = nullptr;
 std::mutex g_mu;
@@ -22,7 +25,7 @@ int check(hipError_t e, const char* what) {
 }
 hipStream_t stream() {
   if (g_device < 0) nqk_init(0);
-  return g_streams[g_device];
+  return g_cur ? g_side[g_device] : g_streams[g_device];
 }
 }  // namespace nqk
 
@@ -72,7 +75,41 @@ int nqk_memset(void* ptr, int value, size_t bytes) {
   if (!bytes) return 0;
   return check(hipMemsetAsync(ptr, value, bytes, stream()), "memset");
 }
-int nqk_sync(void) { return check(hipStreamSynchronize(stream()), "hipStreamSynchronize"); }
+int nqk_sync(void) {
+  if (g_device >= 0 && g_side[g_device] && check(hipStreamSynchronize(g_side[g_device]), "hipStreamSynchronize"))
+    return -1;
+  return check(hipStreamSynchronize(g_device >= 0 ? g_streams[g_device] : stream()), "hipStreamSynchronize");
+}
+
+static int ensure_side() {
+  if (g_device < 0 && nqk_init(0)) return -1;
+  if (!g_side[g_device] &&
+      check(hipStreamCreateWithFlags(&g_side[g_device], hipStreamNonBlocking), "hipStreamCreate"))
+    return -1;
+  if (!g_fork && (check(hipEventCreateWithFlags(&g_fork, hipEventDisableTiming), "hipEventCreate") ||
+                  check(hipEventCreateWithFlags(&g_join, hipEventDisableTiming), "hipEventCreate")))
+    return -1;
+  return 0;
+}
+
+int nqk_set_stream(int which) {
+  if (which != 0 && which != 1) return fail("nqk_set_stream: 0 or 1");
+  if (which == 1 && ensure_side()) return -1;
+  g_cur = which;
+  return 0;
+}
+
+int nqk_stream_fork(void) {
+  if (ensure_side()) return -1;
+  if (check(hipEventRecord(g_fork, g_streams[g_device]), "hipEventRecord")) return -1;
+  return check(hipStreamWaitEvent(g_side[g_device], g_fork, 0), "hipStreamWaitEvent");
+}
+
+int nqk_stream_join(void) {
+  if (ensure_side()) return -1;
+  if (check(hipEventRecord(g_join, g_side[g_device]), "hipEventRecord")) return -1;
+  return check(hipStreamWaitEvent(g_streams[g_device], g_join, 0), "hipStreamWaitEvent");
+}
 int nqk_stream(void** s) { *s = (void*)stream(); return 0; }
 
 int nqk_timer_start(void) { return check(hipEventRecord(g_t0, stream()), "hipEventRecord"); }

@@ -57,6 +57,9 @@ SIGNATURES = {
     "nqk_memset": [_p, _i, ctypes.c_size_t],
     "nqk_sync": [],
     "nqk_stream": [ctypes.POINTER(_p)],
+    "nqk_set_stream": [_i],
+    "nqk_stream_fork": [],
+    "nqk_stream_join": [],
     "nqk_timer_start": [],
     "nqk_timer_stop": [],
     "nqk_timer_ms": [ctypes.POINTER(_f)],

@@ -35,6 +35,7 @@ _EPI_NAMES = {EPI_QKV: "qkv", EPI_SCORES: "scores", EPI_PV: "pv", EPI_RESID: "re
 FUSED_ATTENTION = True
 FUSED_EMBED = True
 LN_GATHER = True
+SPLIT_STREAMS = True
 
 
 Epilogue = _lib.Epilogue
@@ -483,6 +484,7 @@ class FusedLayer:
         # the one-kernel attention covers head size 64, <= 224 tokens and zero points for
         # which every int32 intermediate is exact (nqk.h); otherwise three launches
         zs = [_zp(self.p_head["q"]), _zp(self.p_head["k"]), _zp(self.p_sm), _zp(self.p_head["v"])]
+        self._x1 = None
         self.attn_fused = (FUSED_ATTENTION and m.hdim == 64 and 1 <= m.tokens <= 224 and
                            abs(zs[0]) <= 4096 and abs(zs[1]) <= 4096 and abs(zs[2]) <= 1024 and abs(zs[3]) <= 1024)
 
@@ -526,8 +528,11 @@ class FusedLayer:
                       s_out=[_f32(self.p_ctx.scale)], zp_out=[_zp(self.p_ctx)], out=[w["ctx"].ptr], ld_out=D)
         _gemm(EPI_PV, w["p"], w["vt"], B * H, T, Dh, Tp, Tp, Tp, None, T * Tp, Dh * Tp, e)
 
-    def run(self, ws: "Workspace"):
-        m, bw = self.m, self.bw
+    def run(self, ws: "Workspace", split: bool = False):
+        """The layer on its input value.  split: the images in two halves, one per HIP
+        stream (nqk_set_stream 0 / 1), so each half's kernels fill the other's partial
+        last dispatch rounds; every half touches only its own rows of every buffer."""
+        m = self.m
         x = m.x_in.data
         if isinstance(x, QTensor):  # a quantized graph input: its LN and residual-Add
             x = x.dequantize()      # consumers both see the dequantized tensor (model.py:528-538)
@@ -537,12 +542,42 @@ class FusedLayer:
         if T != m.tokens or D != self.D:
             raise ValueError(f"layer input {x.dev.shape} does not match the graph ({m.tokens}, {self.D})")
         H, Dh, F = m.heads, m.hdim, self.F
-        Mrows = B * T
         Tp = (T + 15) // 16 * 16
         w = ws.get(B, T, Tp, H, Dh, D, F, unfused_attention=not self.attn_fused)
+        # the residual stream buffers stay with the layer: with two streams a buffer
+        # released to the pool could be handed out while the other stream still reads it
+        if self._x1 is None or self._x1.shape != (B, T, D):
+            self._x1 = DeviceArray((B, T, D), np.float32)
+        x2 = DeviceArray((B, T, D), np.float32)
+        if split and self.attn_fused and B >= 2:
+            h = B // 2
+            for s_idx, (i0, nb) in enumerate(((0, h), (h, B - h))):
+                _lib.call("nqk_set_stream", s_idx)
+                self._run_part(w, x.dev, self._x1, x2, i0, nb)
+            _lib.call("nqk_set_stream", 0)
+        else:
+            self._run_part(w, x.dev, self._x1, x2, 0, B)
+        m.x_out.data = FTensor(x2)
+
+    def _run_part(self, w, xd, x1d, x2d, i0, nb):
+        """Images [i0, i0 + nb) of the layer (row views of every buffer)."""
+        m, bw = self.m, self.bw
+        T, D = m.tokens, self.D
+        H, Dh, F = m.heads, m.hdim, self.F
+        Mrows = nb * T
+        Tp = (T + 15) // 16 * 16
+        r0 = i0 * T
+
+        def rows(arr, ncol):
+            return arr.offset_view(r0 * ncol, (Mrows, ncol))
+
+        x, x1, x2 = (rows(t.reshape((t.size // D, D)), D) for t in (xd, x1d, x2d))
+        lnq, ln2q, ctx, hh = rows(w["lnq"], D), rows(w["ln2q"], D), rows(w["ctx"], D), rows(w["h"], F)
+        hq = i0 * H * T * Dh  # head-layout offset of the first image
+        q, k, v = (w[r].offset_view(hq, (nb * H * T, Dh)) for r in "qkv")
         call = _lib.call
         # 1) LN1 + quantize (LN1 output feeds the Q/K/V MatMuls)
-        _ln_quant(x.dev, self.g1, self.be1, w["lnq"], Mrows, D, self.eps1, self.p_ln1, bw)
+        _ln_quant(x, self.g1, self.be1, lnq, Mrows, D, self.eps1, self.p_ln1, bw)
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D, col=self.col_qkv.ptr,
@@ -550,8 +585,8 @@ class FusedLayer:
                       s_acc=[_f32(s_a * np.float32(self.s_w[r])) for r in "qkv"],
                       s_out=[_f32(self.p_head[r].scale) for r in "qkv"],
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
-                      out=[w["q"].ptr, w["k"].ptr, w["v"].ptr], bias=self.bias_qkv.ptr)
-        _gemm(EPI_QKV, w["lnq"], self._b(e, "qkv", self.bt_qkv), 1, Mrows, 3 * D, D, D, D, None, 0, 0, e)
+                      out=[q.ptr, k.ptr, v.ptr], bias=self.bias_qkv.ptr)
+        _gemm(EPI_QKV, lnq, self._b(e, "qkv", self.bt_qkv), 1, Mrows, 3 * D, D, D, D, None, 0, 0, e)
         pq, pk, pv_ = self.p_head["q"], self.p_head["k"], self.p_head["v"]
         if self.attn_fused:
             # 3-6) one kernel per (image, head): scores, softmax, P V, context quantize
@@ -563,32 +598,29 @@ class FusedLayer:
             a.s_pv, a.zv = _f32(np.float32(self.p_sm.scale) * np.float32(pv_.scale)), _zp(pv_)
             a.s_ctx, a.zp_ctx = _f32(self.p_ctx.scale), _zp(self.p_ctx)
             t0 = KM.TIMER.begin() if KM.TIMER is not None else None
-            call("nqk_attention_fused", w["q"].vp, w["k"].vp, w["v"].vp, w["ctx"].vp, B * H, ctypes.byref(a))
+            call("nqk_attention_fused", q.vp, k.vp, v.vp, ctx.vp, nb * H, ctypes.byref(a))
             if t0 is not None:
-                KM.TIMER.end("attention", t0, (2 * 2 * B * H * T * T * Dh, 3 * B * H * T * Dh + B * T * D))
+                KM.TIMER.end("attention", t0, (2 * 2 * nb * H * T * T * Dh, 3 * nb * H * T * Dh + nb * T * D))
         else:
-            self._attention_unfused(w, B, T, Tp, H, Dh, D)
+            self._attention_unfused(w, nb, T, Tp, H, Dh, D)  # whole batch only (i0 == 0)
         # 7) output projection + bias + residual
-        x1 = DeviceArray((B, T, D), np.float32)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr, col_absmax=self.cmax["o"],
                       s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
-                      resid=x.dev.ptr, out=[x1.ptr])
-        _gemm(EPI_RESID, w["ctx"], self._b(e, "o", self.bt_o), 1, Mrows, D, D, D, D, None, 0, 0, e)
+                      resid=x.ptr, out=[x1.ptr])
+        _gemm(EPI_RESID, ctx, self._b(e, "o", self.bt_o), 1, Mrows, D, D, D, D, None, 0, 0, e)
         # 8) LN2 + quantize
-        _ln_quant(x1, self.g2, self.be2, w["ln2q"], Mrows, D, self.eps2, self.p_ln2, bw)
+        _ln_quant(x1, self.g2, self.be2, ln2q, Mrows, D, self.eps2, self.p_ln2, bw)
         # 9) FFN up + bias + GELU + quantize
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr, col_absmax=self.cmax["1"],
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
-                      s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[w["h"].ptr],
+                      s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[hh.ptr],
                       div=m.gelu_div, add1=m.gelu_add, mul2=m.gelu_mul)
-        _gemm(EPI_GELU, w["ln2q"], self._b(e, "1", self.bt_1), 1, Mrows, F, D, D, D, None, 0, 0, e)
+        _gemm(EPI_GELU, ln2q, self._b(e, "1", self.bt_1), 1, Mrows, F, D, D, D, None, 0, 0, e)
         # 10) FFN down + bias + residual
-        x2 = DeviceArray((B, T, D), np.float32)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr, col_absmax=self.cmax["2"],
                       s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
                       resid=x1.ptr, out=[x2.ptr])
-        _gemm(EPI_RESID, w["h"], self._b(e, "2", self.bt_2), 1, Mrows, D, F, F, F, None, 0, 0, e)
-        m.x_out.data = FTensor(x2)
+        _gemm(EPI_RESID, hh, self._b(e, "2", self.bt_2), 1, Mrows, D, F, F, F, None, 0, 0, e)
 
 
 def _pack_b(bt, bit_width=8):
@@ -680,6 +712,8 @@ class Plan:
     def __init__(self, qmodel):
         self.steps = []
         self.ws = Workspace()
+        # fused layers as two half batches on two streams (NQK_SPLIT=0: one stream)
+        self.split = SPLIT_STREAMS and os.environ.get("NQK_SPLIT", "1") != "0"
         self.fused = 0
         claimed = {}
         self.embeds = 0
@@ -736,7 +770,14 @@ class Plan:
                 self.fused += 1
 
     def run(self, qmodel, times=None, profile=False):
+        forked = False
         for kind, obj in self.steps:
+            if kind == "layer" and self.split and not forked:
+                _lib.call("nqk_stream_fork")  # the second stream waits for everything so far
+                forked = True
+            elif kind != "layer" and forked:
+                _lib.call("nqk_stream_join")  # and everything after waits for it
+                forked = False
             if kind == "node":
                 qmodel._run_node(obj, times, profile)
             elif kind == "embed_pre":
@@ -746,7 +787,9 @@ class Plan:
             elif kind == "ln_gather":
                 obj.run(qmodel, times, profile)
             else:
-                obj.run(self.ws)
+                obj.run(self.ws, split=self.split)
+        if forked:
+            _lib.call("nqk_stream_join")
 
 
 def compile_plan(qmodel) -> Plan:
