@@ -364,6 +364,7 @@ class FusedEmbed:
         self.posv = deq(m.pos).dev
         if self.kk % 2 or self.bias.size != self.kout or self.cls.size != self.kout:
             raise NoMatch("embedding dimensions")
+        self._cols = None
 
     def pre(self, qmodel):
         """at the Conv's position: the shape-only placeholder for the Shape consumer"""
@@ -371,31 +372,47 @@ class FusedEmbed:
         n, c, h, w = m.x.data.dev.shape
         m.conv_out.data = _ShapeOnly((n, self.kout, h // m.kh, w // m.kw))
 
-    def run(self, qmodel):
+    def run(self, qmodel, split=False):
+        """split: the images in two halves, one per stream (as FusedLayer.run)."""
         m = self.m
         xd = m.x.data
         n, c, h, w = xd.dev.shape
         ho, wo = h // m.kh, w // m.kw
         hw = ho * wo
         zp = xd.zero_point
-        if isinstance(xd, QTensor) and xd._bias is None and xd.dev.dtype == np.int8 and h % m.kh == 0 and w % m.kw == 0 and \
-                (zp is None or np.ndim(zp) == 0):
-            # dequantize fused into the patch gather (the QTensor is read once, as int8)
-            cols = DeviceArray((n * hw, self.kk), np.float32)
-            _lib.call("nqk_patchify_dequant", xd.dev.vp, cols.vp, n, c, h, w, m.kh, m.kw,
-                      float(np.float32(xd.scale)), int(zp) if zp is not None else 0)
-        else:
-            x = qmodel._dequant_input(m.x) if isinstance(xd, QTensor) else xd
-            cols, ho, wo = KM.im2col(x.dev, m.kh, m.kw, (0, 0, 0, 0), (m.kh, m.kw))
+        fused_in = (isinstance(xd, QTensor) and xd._bias is None and xd.dev.dtype == np.int8 and h % m.kh == 0 and
+                    w % m.kw == 0 and (zp is None or np.ndim(zp) == 0))
         if self.posv.size != (hw + 1) * self.kout:
             raise ValueError("position embedding does not match the patch grid")
         eshape = np.asarray(m.expand.inputs[1].data.data).reshape(-1)
         if eshape.size != 3 or int(eshape[0]) != n:
             raise ValueError(f"class-token Expand shape {eshape} does not match the batch {n}")
         out = DeviceArray((n, hw + 1, self.kout), np.float32)
+        if fused_in:
+            # dequantize fused into the patch gather (the QTensor is read once, as int8); the
+            # patch matrix stays with the step (two streams: see FusedLayer.run)
+            if self._cols is None or self._cols.shape != (n * hw, self.kk):
+                self._cols = DeviceArray((n * hw, self.kk), np.float32)
+            cols = self._cols
+            parts = ((0, n // 2), (n // 2, n - n // 2)) if split and n >= 2 else ((0, n),)
+        else:
+            x = qmodel._dequant_input(m.x) if isinstance(xd, QTensor) else xd
+            cols, ho, wo = KM.im2col(x.dev, m.kh, m.kw, (0, 0, 0, 0), (m.kh, m.kw))
+            parts = ((0, n),)
         t0 = KM.TIMER.begin() if KM.TIMER is not None else None
-        _lib.call("nqk_sgemm_embed", cols.vp, self.wm.vp, self.bias.vp, self.cls.vp, self.posv.vp, out.vp,
-                  n, hw, self.kout, self.kk)
+        for s_idx, (i0, nb) in enumerate(parts):
+            if len(parts) > 1:
+                _lib.call("nqk_set_stream", s_idx)
+            cp = cols.offset_view(i0 * hw * self.kk, (nb * hw, self.kk))
+            if fused_in:
+                qv = xd.dev.offset_view(i0 * c * h * w, (nb, c, h, w))
+                _lib.call("nqk_patchify_dequant", qv.vp, cp.vp, nb, c, h, w, m.kh, m.kw,
+                          float(np.float32(xd.scale)), int(zp) if zp is not None else 0)
+            ov = out.offset_view(i0 * (hw + 1) * self.kout, (nb, hw + 1, self.kout))
+            _lib.call("nqk_sgemm_embed", cp.vp, self.wm.vp, self.bias.vp, self.cls.vp, self.posv.vp, ov.vp,
+                      nb, hw, self.kout, self.kk)
+        if len(parts) > 1:
+            _lib.call("nqk_set_stream", 0)
         if t0 is not None:
             KM.TIMER.end("embed_sgemm", t0, (0, 4 * (n * hw * self.kk + self.kk * self.kout + n * (hw + 1) * self.kout)))
         m.add.outputs[0].data = FTensor(out)
@@ -772,10 +789,10 @@ class Plan:
     def run(self, qmodel, times=None, profile=False):
         forked = False
         for kind, obj in self.steps:
-            if kind == "layer" and self.split and not forked:
+            if kind in ("layer", "embed") and self.split and not forked:
                 _lib.call("nqk_stream_fork")  # the second stream waits for everything so far
                 forked = True
-            elif kind != "layer" and forked:
+            elif kind not in ("layer", "embed") and forked:
                 _lib.call("nqk_stream_join")  # and everything after waits for it
                 forked = False
             if kind == "node":
@@ -783,7 +800,7 @@ class Plan:
             elif kind == "embed_pre":
                 obj.pre(qmodel)
             elif kind == "embed":
-                obj.run(qmodel)
+                obj.run(qmodel, split=self.split)
             elif kind == "ln_gather":
                 obj.run(qmodel, times, profile)
             else:
