@@ -55,16 +55,17 @@ __device__ __forceinline__ float np_expf_t(float x) {
 __device__ __forceinline__ float np_expf(float x) { return np_expf_t<true>(x); }
 
 // np_expf for x <= 0 (including -inf; softmax arguments y - max): no overflow or NaN
-// selects, and without the third Cody-Waite step fma(q, 0, r), which can only turn a -0
-// remainder into +0 and the rational function does not see the sign of a zero.  Equal to
-// np_expf on all 2^31 non-positive inputs (nqk_selftest_fastmath, counts[2]).
+// selects, no zeroing of the argument before the reduction (an underflowing x only
+// produces a value the final select replaces by 0), and without the third Cody-Waite step
+// fma(q, 0, r), which can only turn a -0 remainder into +0 and the rational function does
+// not see the sign of a zero.  Equal to np_expf on all 2^31 non-positive inputs
+// (nqk_selftest_fastmath, counts[2]).
 __device__ __forceinline__ float np_expf_nonpos(float x) {
   const bool under = x <= -103.97208404541015625f;
-  const float xx = under ? 0.0f : x;
-  float q = xx * 1.442695040888963407359924681001892137f;
+  float q = x * 1.442695040888963407359924681001892137f;
   q = q + 0x1.800000p+23f;
   q = q - 0x1.800000p+23f;
-  float r = __builtin_fmaf(q, -6.93145752e-1f, xx);
+  float r = __builtin_fmaf(q, -6.93145752e-1f, x);
   r = __builtin_fmaf(q, -1.42860677e-6f, r);
   float num = __builtin_fmaf(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);
   num = __builtin_fmaf(num, r, 5.114512081637298353406e-02f);
