@@ -167,6 +167,7 @@ def main():
     ap.add_argument("--bit-width", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="node-by-node executor instead of the fused plan")
+    ap.add_argument("--graph", type=int, default=0, help="1: replay the forward as one captured hipGraph")
     args = ap.parse_args()
 
     from numpy_quant import _lib
@@ -193,10 +194,15 @@ def main():
     x_dev = FTensor(x)  # resident in HBM before timing
     logits_all = DeviceArray((world, args.batch, 1000), np.float32) if (world > 1 and rank == 0) else None
 
+    graph = qmodel.graph([x_dev]) if args.graph else None
+
     def step():
-        qmodel.set_inputs([x_dev])
-        qmodel.run()
-        out = qmodel.outputs_device()[0]
+        if graph is not None:
+            out = graph.run_device([x_dev])[0]
+        else:
+            qmodel.set_inputs([x_dev])
+            qmodel.run()
+            out = qmodel.outputs_device()[0]
         group.gather(out.dev, logits_all)
         return out
 
@@ -236,7 +242,7 @@ def main():
                                    f"QModel.__call__, int{args.bit_width}, batch {args.batch}/GPU",
                        "model": "vit_image_classifier_no_weights.onnx (ViT-Base/16-224)",
                        "global_batch": args.batch * world, "seq_len": 197,
-                       "parallelism": f"replicas x{world}", "executor": "eager" if args.eager else "fused plan"},
+                       "parallelism": f"replicas x{world}", "executor": ("eager" if args.eager else "fused plan") + (", hipGraph replay" if graph else "")},
             "matmul_tops": round(achieved, 2),
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(INT8_PEAK_TOPS, 1),
                          "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4),

@@ -78,9 +78,11 @@ int nqk_event_create(void** event);
 int nqk_event_record(void* event);
 int nqk_event_elapsed(void* start, void* stop, float* ms);   /* waits for stop */
 int nqk_event_destroy(void* event);
-/* hipGraph capture of everything issued between begin and end */
+/* hipGraph capture of everything issued between begin and end (relaxed mode: the
+ * caller's allocator may still allocate); abort drops a capture that failed part-way */
 int nqk_graph_begin(void);
 int nqk_graph_end(void** graph_exec);
+int nqk_graph_abort(void);
 int nqk_graph_launch(void* graph_exec);
 int nqk_graph_destroy(void* graph_exec);
 

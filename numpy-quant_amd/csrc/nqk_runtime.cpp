@@ -133,7 +133,24 @@ int nqk_event_elapsed(void* start, void* stop, float* ms) {
 int nqk_event_destroy(void* event) { return check(hipEventDestroy((hipEvent_t)event), "hipEventDestroy"); }
 
 int nqk_graph_begin(void) {
-  return check(hipStreamBeginCapture(stream(), hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+  // relaxed: the caching allocator may still hipMalloc a fresh block mid-capture
+  // (the block lives outside the graph; graph.py pins it for the graph's lifetime)
+  g_cur = 0;
+  return check(hipStreamBeginCapture(stream(), hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+}
+int nqk_graph_abort(void) {
+  // a capture that failed part-way: join the side stream back (it may be part of the
+  // capture after a fork), end the capture and drop the partial graph
+  g_cur = 0;
+  if (g_device >= 0 && g_side[g_device] && g_join) {
+    (void)hipEventRecord(g_join, g_side[g_device]);
+    (void)hipStreamWaitEvent(g_streams[g_device], g_join, 0);
+  }
+  hipGraph_t g = nullptr;
+  (void)hipStreamEndCapture(stream(), &g);
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  return 0;
 }
 int nqk_graph_end(void** graph_exec) {
   hipGraph_t g = nullptr;

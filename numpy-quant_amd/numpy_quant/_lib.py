@@ -69,6 +69,7 @@ SIGNATURES = {
     "nqk_event_destroy": [_p],
     "nqk_graph_begin": [],
     "nqk_graph_end": [ctypes.POINTER(_p)],
+    "nqk_graph_abort": [],
     "nqk_graph_launch": [_p],
     "nqk_graph_destroy": [_p],
     "nqk_quantize": [_p, _p, _i, _l, _f, _l, _i, _i, _p, _l],

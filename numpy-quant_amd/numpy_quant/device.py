@@ -34,6 +34,9 @@ class _Pool:
         self.live_bytes = 0
         self.cached_bytes = 0
         self.peak_bytes = 0
+        # during a hipGraph capture (graph.py) every new block is appended here, so the
+        # graph holds it and the pool never hands it out while the graph can replay
+        self.capture: list | None = None
 
     @staticmethod
     def round(nbytes: int) -> int:
@@ -85,6 +88,8 @@ class _Block:
         _lib.ensure_init()
         self.ptr, self.size = POOL.alloc(max(1, nbytes))
         weakref.finalize(self, POOL.release, self.ptr, self.size)
+        if POOL.capture is not None:
+            POOL.capture.append(self)
 
 
 class DeviceArray:

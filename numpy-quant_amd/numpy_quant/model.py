@@ -421,6 +421,12 @@ class QModel(Model):
         self._plan = compile_plan(self)
         return self._plan
 
+    def graph(self, example_inputs):
+        """Capture one forward on inputs of this shape as a hipGraph (graph.py); the
+        returned DeviceGraph replays it with one launch and the same results."""
+        from .graph import DeviceGraph
+        return DeviceGraph(self, example_inputs)
+
     def _run_node(self, node, times, profile=False):
         """One iteration of the node loop of QModel.__call__ (model.py:502-550)."""
         args = []
