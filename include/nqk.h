@@ -110,6 +110,10 @@ int nqk_requantize(const void* acc, int acc_dtype, const void* bias, int bias_dt
                    const int64_t* row, const int64_t* col, const int64_t* bmap,
                    float res_scale, int64_t res_zp, int has_res_zp, int bit_width);
 
+/* QTensor.relu  tensor.py:212-215:  out[i] = q[i] < zp ? zp : q[i]  (zp the tensor's scalar
+ * zero point; out may be wider than q when zp lies outside q's storage range) */
+int nqk_relu_q(const void* q, int q_dtype, void* out, int out_dtype, int64_t n, int64_t zp);
+
 /* row / column sums of an integer matrix batch (the q_matmul zero-point terms,
  * numpy_quantization.py:52,55,58-59), int64: row[b][m] = sum_k A[b][m][k] (row-major,
  * lda), col[b][n] = sum_k B[b][k][n] (B given TRANSPOSED as Bt[b][n][k], ldb). */

@@ -163,6 +163,16 @@ __global__ void k_rowsum(const T* __restrict__ a, int64_t* __restrict__ out, int
   }
 }
 
+// QTensor.relu (tensor.py:212-215): q < zp -> zp, elementwise, any storage in / out
+template <typename TI, typename TO>
+__global__ void k_relu_q(const TI* __restrict__ q, TO* __restrict__ out, int64_t n, int64_t zp) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t v = (int64_t)q[i];
+    out[i] = (TO)(v < zp ? zp : v);
+  }
+}
+
 QuantP make_qp(float scale, int64_t zp, int has_zp, int bw) {
   QuantP p;
   p.scale = scale;
@@ -247,4 +257,13 @@ extern "C" int nqk_rowsum(const void* a, int dtype, int64_t* out, int64_t batch,
   NQK_INT_DISPATCH(dtype, T, hipLaunchKernelGGL(k_rowsum<T>, dim3(g), dim3(kThreads), 0, stream(),
                                                   (const T*)a, out, batch, rows, k, ld, batch_stride));
   return launch_status("nqk_rowsum");
+}
+
+extern "C" int nqk_relu_q(const void* q, int q_dtype, void* out, int out_dtype, int64_t n, int64_t zp) {
+  if (n <= 0) return 0;
+  unsigned g = grid_for(n);
+  NQK_INT_DISPATCH(q_dtype, TI,
+    NQK_INT_DISPATCH(out_dtype, TO,
+      hipLaunchKernelGGL((k_relu_q<TI, TO>), dim3(g), dim3(kThreads), 0, stream(), (const TI*)q, (TO*)out, n, zp)));
+  return launch_status("nqk_relu_q");
 }

@@ -76,6 +76,7 @@ SIGNATURES = {
     "nqk_dequantize": [_p, _i, _p, _l, _l, _l, _f, _i, _l, _l, _l, _l, _p, _p, _lp],
     "nqk_requantize": [_p, _i, _p, _i, _p, _i, _l, _l, _l, _f, _i, _l, _l, _l, _l, _p, _p, _lp, _f, _l, _i, _i],
     "nqk_rowsum": [_p, _i, _p, _l, _l, _l, _l, _l],
+    "nqk_relu_q": [_p, _i, _p, _i, _l, _l],
     "nqk_qgemm_i8": [_p, _p, _p, _l, _l, _l, _l, _l, _l, _l, _lp, _l, _l, _l],
     "nqk_qgemm_generic": [_p, _i, _p, _i, _p, _l, _l, _l, _l, _l, _l, _l, _l, _l, _lp, _l, _l, _l],
     "nqk_sgemm": [_p, _p, _p, _l, _l, _l, _l, _l, _l, _l, _l, _l, _lp, _l, _l, _l],

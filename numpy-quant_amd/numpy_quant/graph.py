@@ -13,7 +13,12 @@ Lifetime rules (why replay is safe):
   * every block allocated during capture is held by the graph (the pool's capture
     list), so no buffer the graph writes is handed to anyone else while it lives;
   * replay copies the new inputs into the captured input buffers and returns the
-    captured output buffers, which the next replay overwrites.
+    captured output buffers, which the next replay overwrites.  The qmodel's own
+    values alias the graph's buffers after capture: every replay overwrites them,
+    until the model's next eager or plan run assigns fresh ones.
+  * host state read while capturing (epilogue parameters, shapes, scales) is frozen
+    into the graph; kernel timers (kernels.TIMER) would be too, so capture refuses
+    to run while one is active.
 Integer (int64) model inputs are host tensors in this design and would be baked into
 the graph, so they are refused.
 """
@@ -35,6 +40,9 @@ class DeviceGraph:
 
     def __init__(self, qmodel, example_inputs: Sequence[Union[np.ndarray, FTensor]]):
         _lib.ensure_init()
+        from . import kernels as KM
+        if KM.TIMER is not None:
+            raise RuntimeError("DeviceGraph: kernels.TIMER is active; its events would be frozen into the graph")
         self.q = qmodel
         self.staging: List[FTensor] = []
         for a in example_inputs:
@@ -45,7 +53,7 @@ class DeviceGraph:
             else:
                 raise ValueError("DeviceGraph: float32 inputs only (int64 inputs are host tensors)")
         self.plan = None
-        if qmodel._plan is not None:
+        if qmodel._plan is not None or (qmodel.fuse and not qmodel.keep_values):
             from .plan import compile_plan
             self.plan = compile_plan(qmodel)
         self.exec = ctypes.c_void_p()
@@ -73,7 +81,7 @@ class DeviceGraph:
 
     def _forward(self) -> List[FTensor]:
         self.q.set_inputs(self.staging)
-        self.q.run()
+        self.q.run(eager=self.plan is None)
         return self.q.outputs_device()
 
     def _load(self, inputs) -> None:

@@ -180,18 +180,20 @@ class KernelTimer:
         _lib.call("nqk_event_record", e)
         return e
 
-    def end(self, tag, start, work):
+    def end(self, tag, start, work, unit="int8"):
+        """work = (ops, algorithmic bytes); unit: what the ops count ("int8" MFMA ops,
+        "flop32" f32 MFMA flops)."""
         e = self._event()
         _lib.call("nqk_event_record", e)
-        self.records.append((tag, start, e, work))
+        self.records.append((tag, start, e, work, unit))
 
     def collect(self):
-        """[(tag, ms, work)] and recycle the events."""
+        """[(tag, ms, work, unit)] and recycle the events."""
         out = []
-        for tag, a, b, w in self.records:
+        for tag, a, b, w, unit in self.records:
             ms = ctypes.c_float()
             _lib.call("nqk_event_elapsed", a, b, ctypes.byref(ms))
-            out.append((tag, ms.value, w))
+            out.append((tag, ms.value, w, unit))
             self._free += [a, b]
         self.records = []
         return out

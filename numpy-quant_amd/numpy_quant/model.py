@@ -6,8 +6,10 @@ The node loop is the reference's (model.py:294-326, 486-565): per node, QTensor
 inputs of float ops are dequantized, float inputs of MatMul / Gemm are quantized
 with the calibrated parameters, Gemm outputs are requantized.  All intermediate
 values stay in HBM; `value.data.data` copies one to the host on request.
-`QModel.compile()` additionally offers a fused device plan (plan.py) with
-bit-identical results for the hot MatMul chains.
+`QModel.__call__` runs through a fused device plan (plan.py, compiled on first
+use) with bit-identical results for the hot MatMul chains; `qmodel.keep_values = True`
+(or `profile=True`) keeps the reference's node-by-node loop, which materialises every
+intermediate `value.data`.
 """
 from __future__ import annotations
 
@@ -295,7 +297,25 @@ class Model:
         skipping the calibration forward."""
         return self._rewrite(bit_width, lambda value, asym: quant_params[value.name])
 
-    def _rewrite(self, bit_width, params):
+    def load_quantized(self, path):
+        """The QModel saved by `QModel.save(path)` (blob.py) on this model's graph:
+        no calibration forward and no constant re-quantization."""
+        from . import blob
+        return blob.load(self, path)
+
+    def _rewrite(self, bit_width, params, constants=None):
+        """model.py:338-442.  `constants`: name -> ready quantized QTensor (blob.py);
+        those constants are taken as they are instead of being quantized here."""
+        constants = constants or {}
+        wanted = {}
+
+        def qconst(value, bw, scale, zp):
+            t = constants.get(value.name)
+            if t is None:
+                return quantize_tensor(value.data, bw, scale, zp)
+            wanted[value.name] = bw  # a bias is quantized at bw, then again at 4*bw: last wins
+            return t
+
         node_dict = {node.name: node for node in self.nodes}
         value_dict = {value.name: value for value in self.values}
 
@@ -308,7 +328,7 @@ class Model:
         for value in self.values:
             if isinstance(value, Constant):
                 p = params(value, False)
-                qt = quantize_tensor(value.data, bit_width, p.scale, p.zero_point)
+                qt = qconst(value, bit_width, p.scale, p.zero_point)
                 qt._is_weight = True
                 qvalues[value.name] = Constant(value.name, [], qt)
                 qp[value.name] = p
@@ -326,7 +346,7 @@ class Model:
                 bias = node.inputs[2]
                 bscale = qp[node.inputs[0].name].scale * qp[node.inputs[1].name].scale
                 qp[bias.name] = QuantizationParams(bscale, None)
-                qvalues[bias.name] = Constant(bias.name, [], quantize_tensor(bias.data, 4 * bit_width, bscale, None))
+                qvalues[bias.name] = Constant(bias.name, [], qconst(bias, 4 * bit_width, bscale, None))
                 qnodes[node.name] = Node(node.name, "Gemm", node.attrs, [], [])
                 qp[out_val.name] = params(out_val, True)
                 qvalues[out_val.name] = Variable(out_val.name, [], [], None)
@@ -334,7 +354,7 @@ class Model:
                 bi, xi = (0, 1) if isinstance(node.inputs[0], Constant) else (1, 0)
                 bname = node.inputs[bi].name
                 bscale = qp[node.inputs[xi].name].scale
-                qvalues[bname] = Constant(bname, [], quantize_tensor(node.inputs[bi].data, 4 * bit_width, bscale, None))
+                qvalues[bname] = Constant(bname, [], qconst(node.inputs[bi], 4 * bit_width, bscale, None))
                 qp[bname] = QuantizationParams(bscale, None)
                 qnodes[node.name] = Node(node.name, "Add", node.attrs, [], [])
                 qp[out_val.name] = params(out_val, True)
@@ -354,6 +374,9 @@ class Model:
             if isinstance(qvalue, Variable):
                 qvalue.inputs = [qnodes[i.name] for i in value_dict[name].inputs]
             qvalue.outputs = [qnodes[o.name] for o in value_dict[name].outputs]
+        for name, bw in wanted.items():
+            if qvalues[name].data.bit_width != bw:
+                raise ValueError(f"blob constant {name}: bit width {qvalues[name].data.bit_width}, the graph needs {bw}")
         qoutputs = [qvalues[o.name] for o in self.outputs]
         qinputs = [qvalues[i.name] for i in self.inputs]
         return QModel(list(qnodes.values()), list(qvalues.values()), qinputs, qoutputs, bit_width, qp)
@@ -366,6 +389,11 @@ class QModel(Model):
         self.quant_params = quant_params
         self._deq_cache: dict[str, FTensor] = {}
         self._plan = None
+        # QModel.__call__ compiles the fused plan on first use (NQK_FUSE=0: never);
+        # keep_values = True runs the reference's node loop instead, so every
+        # intermediate value.data is populated (reference test/test_mlp.py:159-168)
+        self.fuse = os.environ.get("NQK_FUSE", "1") != "0"
+        self.keep_values = False
 
     def __repr__(self):
         return (f"QModel(nodes={self.nodes}, values={self.values}, inputs={self.inputs}, outputs={self.values}, "
@@ -421,6 +449,12 @@ class QModel(Model):
         self._plan = compile_plan(self)
         return self._plan
 
+    def save(self, path) -> int:
+        """Write the packed quantized constants + every QuantizationParams (blob.py);
+        `Model.load_quantized(path)` rebuilds this QModel on the same graph."""
+        from . import blob
+        return blob.save(self, path)
+
     def graph(self, example_inputs):
         """Capture one forward on inputs of this shape as a hipGraph (graph.py); the
         returned DeviceGraph replays it with one launch and the same results."""
@@ -465,13 +499,13 @@ class QModel(Model):
         for o, tensor in zip(node.outputs, outs):
             o.data = tensor
 
-    def run(self, profile=False):
+    def run(self, profile=False, eager=False):
         """The node loop of QModel.__call__ (model.py:497-550) on device tensors,
-        through the fused plan when `compile()` was called."""
+        through the fused plan when one was compiled (and not `eager`)."""
         times = {op: 0.0 for op in {n.op for n in self.nodes}}
         times["TinyqQuant"] = 0.0
         times["TinyqDequant"] = 0.0
-        if self._plan is not None:
+        if self._plan is not None and not eager:
             self._plan.run(self, times, profile)
         else:
             for node in self.nodes:
@@ -491,8 +525,13 @@ class QModel(Model):
         return res
 
     def __call__(self, inputs: List[np.ndarray], profile=False):
-        """QModel.__call__ (model.py:486-565)."""
+        """QModel.__call__ (model.py:486-565).  The fused plan (bit-identical) unless
+        keep_values is set or a per-op profile is asked for (profile=True returns the
+        reference's {op_type: seconds} dict, which needs the node loop)."""
+        eager = self.keep_values or profile
+        if not eager and self._plan is None and self.fuse:
+            self.compile()
         self.set_inputs(inputs)
-        times = self.run(profile=profile)
+        times = self.run(profile=profile, eager=eager)
         outs = [t.data for t in self.outputs_device()]
         return (outs, times) if profile else outs

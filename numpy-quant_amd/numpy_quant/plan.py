@@ -41,6 +41,51 @@ SPLIT_STREAMS = True
 Epilogue = _lib.Epilogue
 
 
+class Streams:
+    """Fork / join bookkeeping of Plan.run's two HIP streams.
+
+    A split step runs its images in two halves, half 0 on stream 0 and half 1 on
+    stream 1 (nqk_set_stream); consecutive split steps use the same halves, so each
+    stream only depends on its own earlier work and no event is needed between them.
+    Whole-batch work (eager nodes, a dequantized layer input, an unsplit layer) must
+    first `join()` (stream 0 waits for stream 1); halves that follow whole-batch work
+    on stream 0 must first `fork()` (stream 1 waits for stream 0)."""
+
+    def __init__(self, enabled: bool):
+        self.enabled = enabled
+        self.forked = False
+
+    def fork(self):
+        if not self.forked:
+            _lib.call("nqk_stream_fork")
+            self.forked = True
+
+    def join(self):
+        if self.forked:
+            _lib.call("nqk_stream_join")
+            self.forked = False
+
+    def halves(self, n: int, fn):
+        """fn(stream_index, first_image, images) for the two halves of n images on the
+        two streams (or once, whole batch on stream 0, when splitting is off / n < 2);
+        the current stream is back to 0 afterwards, also when fn raises."""
+        if not self.enabled or n < 2:
+            self.join()
+            fn(0, 0, n)
+            return
+        self.fork()
+        h = n // 2
+        try:
+            for s_idx, (i0, nb) in enumerate(((0, h), (h, n - h))):
+                _lib.call("nqk_set_stream", s_idx)
+                fn(s_idx, i0, nb)
+        finally:
+            _lib.call("nqk_set_stream", 0)
+
+
+_ONE_STREAM = Streams(False)
+
+
 class NoMatch(Exception):
     pass
 
@@ -372,8 +417,9 @@ class FusedEmbed:
         n, c, h, w = m.x.data.dev.shape
         m.conv_out.data = _ShapeOnly((n, self.kout, h // m.kh, w // m.kw))
 
-    def run(self, qmodel, split=False):
-        """split: the images in two halves, one per stream (as FusedLayer.run)."""
+    def run(self, qmodel, streams: Streams = _ONE_STREAM):
+        """The embedding of every image; with splitting on, in two halves, one per
+        stream (as FusedLayer.run)."""
         m = self.m
         xd = m.x.data
         n, c, h, w = xd.dev.shape
@@ -394,15 +440,14 @@ class FusedEmbed:
             if self._cols is None or self._cols.shape != (n * hw, self.kk):
                 self._cols = DeviceArray((n * hw, self.kk), np.float32)
             cols = self._cols
-            parts = ((0, n // 2), (n // 2, n - n // 2)) if split and n >= 2 else ((0, n),)
         else:
+            streams.join()  # whole-batch dequantize / im2col on stream 0
             x = qmodel._dequant_input(m.x) if isinstance(xd, QTensor) else xd
             cols, ho, wo = KM.im2col(x.dev, m.kh, m.kw, (0, 0, 0, 0), (m.kh, m.kw))
-            parts = ((0, n),)
+            streams = _ONE_STREAM
         t0 = KM.TIMER.begin() if KM.TIMER is not None else None
-        for s_idx, (i0, nb) in enumerate(parts):
-            if len(parts) > 1:
-                _lib.call("nqk_set_stream", s_idx)
+
+        def part(s_idx, i0, nb):
             cp = cols.offset_view(i0 * hw * self.kk, (nb * hw, self.kk))
             if fused_in:
                 qv = xd.dev.offset_view(i0 * c * h * w, (nb, c, h, w))
@@ -411,10 +456,12 @@ class FusedEmbed:
             ov = out.offset_view(i0 * (hw + 1) * self.kout, (nb, hw + 1, self.kout))
             _lib.call("nqk_sgemm_embed", cp.vp, self.wm.vp, self.bias.vp, self.cls.vp, self.posv.vp, ov.vp,
                       nb, hw, self.kout, self.kk)
-        if len(parts) > 1:
-            _lib.call("nqk_set_stream", 0)
+
+        streams.halves(n, part)
         if t0 is not None:
-            KM.TIMER.end("embed_sgemm", t0, (0, 4 * (n * hw * self.kk + self.kk * self.kout + n * (hw + 1) * self.kout)))
+            KM.TIMER.end("embed_sgemm", t0, (2 * n * hw * self.kk * self.kout,
+                                             4 * (n * hw * self.kk + self.kk * self.kout + n * (hw + 1) * self.kout)),
+                         unit="flop32")
         m.add.outputs[0].data = FTensor(out)
         m.conv_out.data = None
 
@@ -501,7 +548,6 @@ class FusedLayer:
         # the one-kernel attention covers head size 64, <= 224 tokens and zero points for
         # which every int32 intermediate is exact (nqk.h); otherwise three launches
         zs = [_zp(self.p_head["q"]), _zp(self.p_head["k"]), _zp(self.p_sm), _zp(self.p_head["v"])]
-        self._x1 = None
         self.attn_fused = (FUSED_ATTENTION and m.hdim == 64 and 1 <= m.tokens <= 224 and
                            abs(zs[0]) <= 4096 and abs(zs[1]) <= 4096 and abs(zs[2]) <= 1024 and abs(zs[3]) <= 1024)
 
@@ -545,14 +591,15 @@ class FusedLayer:
                       s_out=[_f32(self.p_ctx.scale)], zp_out=[_zp(self.p_ctx)], out=[w["ctx"].ptr], ld_out=D)
         _gemm(EPI_PV, w["p"], w["vt"], B * H, T, Dh, Tp, Tp, Tp, None, T * Tp, Dh * Tp, e)
 
-    def run(self, ws: "Workspace", split: bool = False):
-        """The layer on its input value.  split: the images in two halves, one per HIP
-        stream (nqk_set_stream 0 / 1), so each half's kernels fill the other's partial
-        last dispatch rounds; every half touches only its own rows of every buffer."""
+    def run(self, ws: "Workspace", streams: Streams = _ONE_STREAM):
+        """The layer on its input value.  With splitting on, the images in two halves,
+        one per HIP stream, so each half's kernels fill the other's partial last dispatch
+        rounds; every half touches only its own rows of every buffer."""
         m = self.m
         x = m.x_in.data
         if isinstance(x, QTensor):  # a quantized graph input: its LN and residual-Add
-            x = x.dequantize()      # consumers both see the dequantized tensor (model.py:528-538)
+            streams.join()          # consumers both see the dequantized tensor (model.py:528-538),
+            x = x.dequantize()      # computed whole-batch on stream 0
         if not isinstance(x, FTensor):
             raise ValueError("fused layer input must be a float or quantized tensor")
         B, T, D = x.dev.shape
@@ -561,19 +608,13 @@ class FusedLayer:
         H, Dh, F = m.heads, m.hdim, self.F
         Tp = (T + 15) // 16 * 16
         w = ws.get(B, T, Tp, H, Dh, D, F, unfused_attention=not self.attn_fused)
-        # the residual stream buffers stay with the layer: with two streams a buffer
-        # released to the pool could be handed out while the other stream still reads it
-        if self._x1 is None or self._x1.shape != (B, T, D):
-            self._x1 = DeviceArray((B, T, D), np.float32)
+        # x1 is layer-private scratch shared by all layers (halves touch disjoint rows);
+        # x2 is the layer's output value
         x2 = DeviceArray((B, T, D), np.float32)
-        if split and self.attn_fused and B >= 2:
-            h = B // 2
-            for s_idx, (i0, nb) in enumerate(((0, h), (h, B - h))):
-                _lib.call("nqk_set_stream", s_idx)
-                self._run_part(w, x.dev, self._x1, x2, i0, nb)
-            _lib.call("nqk_set_stream", 0)
-        else:
-            self._run_part(w, x.dev, self._x1, x2, 0, B)
+        if not self.attn_fused:
+            streams.join()  # the three-launch attention runs whole-batch on stream 0
+            streams = _ONE_STREAM
+        streams.halves(B, lambda s_idx, i0, nb: self._run_part(w, x.dev, w["x1"], x2, i0, nb))
         m.x_out.data = FTensor(x2)
 
     def _run_part(self, w, xd, x1d, x2d, i0, nb):
@@ -713,6 +754,7 @@ class Workspace:
                 "q": DeviceArray((B * H * T, Dh), np.int8), "k": DeviceArray((B * H * T, Dh), np.int8),
                 "v": DeviceArray((B * H * T, Dh), np.int8),
                 "ctx": DeviceArray((M, D), np.int8), "h": DeviceArray((M, F), np.int8),
+                "x1": DeviceArray((B, T, D), np.float32),
             }
             self.key = key
         if unfused_attention and "s" not in self.bufs:
@@ -787,26 +829,24 @@ class Plan:
                 self.fused += 1
 
     def run(self, qmodel, times=None, profile=False):
-        forked = False
-        for kind, obj in self.steps:
-            if kind in ("layer", "embed") and self.split and not forked:
-                _lib.call("nqk_stream_fork")  # the second stream waits for everything so far
-                forked = True
-            elif kind not in ("layer", "embed") and forked:
-                _lib.call("nqk_stream_join")  # and everything after waits for it
-                forked = False
-            if kind == "node":
-                qmodel._run_node(obj, times, profile)
-            elif kind == "embed_pre":
-                obj.pre(qmodel)
-            elif kind == "embed":
-                obj.run(qmodel, split=self.split)
-            elif kind == "ln_gather":
-                obj.run(qmodel, times, profile)
-            else:
-                obj.run(self.ws, split=self.split)
-        if forked:
-            _lib.call("nqk_stream_join")
+        streams = Streams(self.split)
+        try:
+            for kind, obj in self.steps:
+                if kind == "node":
+                    streams.join()  # everything eager waits for both streams
+                    qmodel._run_node(obj, times, profile)
+                elif kind == "embed_pre":
+                    obj.pre(qmodel)  # host only: a shape placeholder
+                elif kind == "embed":
+                    obj.run(qmodel, streams)
+                elif kind == "ln_gather":
+                    streams.join()
+                    obj.run(qmodel, times, profile)
+                else:
+                    obj.run(self.ws, streams)
+        finally:
+            _lib.call("nqk_set_stream", 0)
+            streams.join()
 
 
 def compile_plan(qmodel) -> Plan:

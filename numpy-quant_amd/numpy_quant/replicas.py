@@ -4,12 +4,11 @@ The quantized forward has no exchange step — images are independent — so N G
 run N replicas of the same QModel on their own batches (weak scaling).  What is
 shared is set up once:
 
-* calibration runs on rank 0 only; its per-value (min, max) are broadcast over the
-  control plane, so every rank derives bit-identical QuantizationParams
-  (numpy_quantization.quant_parameters is deterministic host arithmetic);
-* the quantized constants (packed int8 weights, int64/f32 biases) are broadcast
-  from rank 0's HBM over RCCL (xGMI) before the plan is compiled, so rank 0's
-  weights are the single source of truth;
+* calibration and quantization run on rank 0 only; its QModel — every quantized
+  constant in one contiguous device buffer plus every QuantizationParams (blob.py)
+  — reaches the other ranks as ONE RCCL broadcast over xGMI (the blob header, a few
+  hundred KB of JSON, goes over the control plane), so rank 0's model is the single
+  source of truth and no other rank calibrates;
 * per step, each rank's logits are gathered into rank 0's HBM over RCCL.
 
 The control plane is torch.distributed with the gloo backend (CPU): rendezvous,
@@ -22,6 +21,12 @@ import ctypes
 import os
 
 import numpy as np
+
+
+def check_gather_sizes(rank: int, world: int, src_bytes: int, dst_bytes) -> None:
+    """rank 0 gathers world * src bytes; raise before any collective is issued."""
+    if rank == 0 and (dst_bytes is None or dst_bytes != world * src_bytes):
+        raise ValueError(f"gather: rank 0 needs a destination of {world} x {src_bytes} bytes, got {dst_bytes}")
 
 
 class ReplicaGroup:
@@ -84,9 +89,35 @@ class ReplicaGroup:
         _lib.call("nqk_comm_init", uid, self.world, self.rank)
         self.device_comm = True
 
+    def broadcast_qmodel(self, model, qmodel=None):
+        """Rank 0 passes its QModel; every rank returns (qmodel, payload bytes): rank 0
+        its own, the others one built on `model`'s graph from rank 0's blob, received
+        with a single ncclBroadcast of the packed payload."""
+        if self.world == 1:
+            return qmodel, 0
+        from . import _lib, blob
+        from .device import DeviceArray
+        if self.rank == 0 and qmodel is None:
+            raise ValueError("broadcast_qmodel: rank 0 must supply its QModel")
+        self.init_device_comm()
+        header = payload = None
+        if self.rank == 0:
+            header, payload = blob.pack(qmodel)
+        header = self.broadcast_object(header)
+        n = int(header["payload_bytes"])
+        if self.rank != 0:
+            payload = DeviceArray((max(n, 1),), np.uint8)
+        if n:
+            _lib.call("nqk_comm_bcast", payload.vp, n, 0)
+        _lib.call("nqk_sync")
+        if self.rank == 0:
+            return qmodel, n
+        return blob.attach(model, header, payload), n
+
     def broadcast_constants(self, qmodel) -> int:
-        """Broadcast every device-resident constant of `qmodel` from rank 0 (call
-        before QModel.compile(), which packs weights from these buffers)."""
+        """Broadcast every device-resident constant of `qmodel` from rank 0, one
+        collective per constant (kept for models built on every rank; bench.py uses
+        broadcast_qmodel's single blob broadcast)."""
         if self.world == 1:
             return 0
         from . import _lib
@@ -105,8 +136,7 @@ class ReplicaGroup:
         if self.world == 1:
             return
         from . import _lib
-        if self.rank == 0 and (dst is None or dst.nbytes != self.world * src.nbytes):
-            raise ValueError("gather: rank 0 needs a destination of world * src bytes")
+        check_gather_sizes(self.rank, self.world, src.nbytes, None if dst is None else dst.nbytes)
         _lib.call("nqk_comm_gather", src.vp, dst.vp if self.rank == 0 else None, src.nbytes, 0)
 
     def close(self) -> None:

@@ -299,9 +299,23 @@ class QTensor:
         return QTensor(acc, 4 * self.bit_width, scale, zt)
 
     def relu(self):
-        # tensor.py:284-287 is never reached from QModel (model.py:528-538 dequantizes
-        # first); SURVEY.md §2 marks it out of scope for the device backend.
-        raise NotImplementedError("QTensor.relu is not on the QModel path")
+        """tensor.py:212-215: values below the zero point become the zero point (the
+        dequantized value is clamped at 0).  The reference compares with a scalar zero
+        point; without one its comparison with None raises TypeError, and so does this."""
+        zp = self._zero_point
+        if zp is None:
+            raise TypeError("'<' not supported between instances of 'numpy.ndarray' and 'NoneType'")
+        if isinstance(zp, K.ZpTerm) or self._bias is not None:
+            raise ValueError("relu of a q_matmul accumulator is not on the QModel path")
+        zp = int(zp)
+        st = self.dev.dtype
+        info = np.iinfo(st)
+        if not (info.min <= zp <= info.max):
+            st = np.dtype(np.int64)  # the zero point itself must be storable
+        out = DeviceArray(self.dev.shape, st)
+        from .device import dtype_code
+        _lib.call("nqk_relu_q", self.dev.vp, dtype_code(self.dev.dtype), out.vp, dtype_code(st), self.dev.size, zp)
+        return QTensor(out, self.bit_width, self.scale, self._zero_point)
 
     def sigmoid(self):
         act = self.dequantize().sigmoid()

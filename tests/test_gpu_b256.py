@@ -1,0 +1,78 @@
+"""GPU parity at the benchmarked size (BASELINE configs[2] / configs[4]): ViT-Base at
+batch 256 through QModel.__call__ (fused plan, two half-batch streams, the GEMMs'
+ragged last tiles and XCD tile order at M = 50 432 rows).
+
+With fixed quantization parameters every op of the quantized forward is per image, so
+  * image 0, the reference fixture's image, must give the reference's logits
+    (tests/golden/vit_b1.npz, recorded from the reference's own QModel.__call__,
+    model.py:486-565) bit for bit, and
+  * the images at both ends of the two stream halves must equal a batch-1 run of the
+    same image through the node-by-node loop (itself pinned to the reference by
+    tests/test_gpu_models.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+B = 256
+CHECK = (0, 1, B // 2 - 1, B // 2, B - 1)
+
+
+def _batch(seed_image):
+    rng = np.random.default_rng(2560)
+    x = rng.standard_normal((B, 3, 224, 224)).astype(np.float32)
+    x[0] = seed_image[0]
+    return x
+
+
+def _eager_rows(model, qmodel, x, rows):
+    model.rebatch(1)
+    qmodel.keep_values = True
+    try:
+        return {i: qmodel([x[i:i + 1]])[0][0] for i in rows}
+    finally:
+        qmodel.keep_values = False
+        model.rebatch(B)
+
+
+def test_vit_b256_int8_matches_reference_fixture():
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model
+    from test_gpu_models import ref_qparams
+    meta = json.load(open(os.path.join(GOLDEN, "vit_b1.json")))
+    arrs = np.load(os.path.join(GOLDEN, "vit_b1.npz"))
+    proto = onnx_proto.load(os.path.join(ROOT, "numpy-quant_amd", "models", "vit_image_classifier_no_weights.onnx"),
+                            synthetic_weights=True, seed=meta["seed"])
+    model = Model.from_onnx(proto)
+    model.rebatch(B)
+    qmodel = model.quantize_with(ref_qparams(meta["bw8"]["qparams"]), bit_width=8)
+    x = _batch(arrs["x_run"])
+    out = qmodel([x])[0]
+    plan = qmodel._plan
+    assert plan is not None and plan.split and plan.fused == 12 and plan.embeds == 1
+    np.testing.assert_array_equal(out[0], arrs["bw8_out"][0])
+    for i, ref in _eager_rows(model, qmodel, x, CHECK[1:]).items():
+        np.testing.assert_array_equal(out[i], ref, err_msg=f"image {i}")
+
+
+def test_vit_b256_int4_matches_batch1_node_loop():
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model
+    arrs = np.load(os.path.join(GOLDEN, "vit_b1.npz"))
+    proto = onnx_proto.load(os.path.join(ROOT, "numpy-quant_amd", "models", "vit_image_classifier_no_weights.onnx"),
+                            synthetic_weights=True)
+    model = Model.from_onnx(proto)
+    qmodel = model.quantize([arrs["x_cal"]], bit_width=4)  # batch-1 device calibration
+    model.rebatch(B)
+    x = _batch(arrs["x_run"])
+    out = qmodel([x])[0]
+    plan = qmodel._plan
+    assert plan.fused == 12
+    # the nibble-packed int4 weight images are in use
+    assert all(layer.bp["1"][1] == 2 for kind, layer in plan.steps if kind == "layer")
+    for i, ref in _eager_rows(model, qmodel, x, CHECK).items():
+        np.testing.assert_array_equal(out[i], ref, err_msg=f"image {i}")

@@ -151,6 +151,7 @@ def test_vit_graphs_bit_exact(tag, fname, batch):
             np.testing.assert_array_equal(out, arrs[f"{bw_key}_out"])
         # 2) QModel.__call__ with the reference's quantization parameters: bit-exact
         qmodel = model.quantize_with(ref_qparams(meta[bw_key]["qparams"]), bit_width=bw)
+        qmodel.keep_values = True  # the node loop: every intermediate value is checked
         out = qmodel([arrs["x_run"]])[0]
         np.testing.assert_array_equal(out, arrs[f"{bw_key}_out"])
         hashes = meta[bw_key]["hashes"]

@@ -47,7 +47,9 @@ def test_plan_equals_eager(batch, bw):
     x = rng.standard_normal((batch, 3, 224, 224)).astype(np.float32)
     model = _vit(batch)
     qmodel = model.quantize([x], bit_width=bw)
+    qmodel.keep_values = True
     eager = qmodel([x])[0]
+    qmodel.keep_values = False
     layer_outs = {}
     plan = qmodel.compile()
     assert plan.fused == 12 and plan.embeds == 1 and plan.pushdowns == 1
@@ -71,7 +73,78 @@ def test_plan_encoder_layer_graph_matches_oracle():
         ref = O.outputs_of(graph, O.quantized_forward(graph, qp, qc, [x], 8))[0]
     model = Model.from_onnx(onnx_proto.load(path, synthetic_weights=True))
     qmodel = model.quantize_with({k: QuantizationParams(v.scale, v.zero_point) for k, v in qp.items()}, bit_width=8)
+    qmodel.keep_values = True
     np.testing.assert_array_equal(qmodel([x])[0], ref)
+    qmodel.keep_values = False
     plan = qmodel.compile()
     assert plan.fused == 1
     np.testing.assert_array_equal(qmodel([x])[0], ref)
+
+
+def _split_vs_one_stream(qmodel, x):
+    plan = qmodel.compile()
+    assert plan.split
+    two = qmodel([x])[0]
+    plan.split = False
+    one = qmodel([x])[0]
+    plan.split = True
+    return plan, two, one
+
+
+def test_plan_split_with_unsplit_layers(monkeypatch):
+    """Split embedding followed by layers that run whole-batch (three-launch attention):
+    the layers must wait for both embedding halves (plan.Streams.join)."""
+    from numpy_quant import plan as P
+    monkeypatch.setattr(P, "FUSED_ATTENTION", False)
+    x = np.random.default_rng(11).standard_normal((3, 3, 224, 224)).astype(np.float32)
+    model = _vit(3)
+    qmodel = model.quantize([x], bit_width=8)
+    qmodel.keep_values = True
+    eager = qmodel([x])[0]
+    qmodel.keep_values = False
+    plan, two, one = _split_vs_one_stream(qmodel, x)
+    assert plan.fused == 12 and not any(l.attn_fused for k, l in plan.steps if k == "layer")
+    np.testing.assert_array_equal(two, eager)
+    np.testing.assert_array_equal(one, eager)
+
+
+def test_plan_encoder_layer_graph_batch2_split():
+    """A quantized graph input feeding a split layer: its whole-batch dequantize on
+    stream 0 must precede the stream-1 half (fork after the dequantize)."""
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model
+    path = os.path.join(MODELS, "vit_image_classifier_encoder_layer_no_weights.onnx")
+    x = np.random.default_rng(6).standard_normal((2, 197, 768)).astype(np.float32)
+    proto = onnx_proto.load(path, synthetic_weights=True)
+    onnx_proto.rebatch(proto, 2)
+    qmodel = Model.from_onnx(proto).quantize([x], bit_width=8)
+    qmodel.keep_values = True
+    eager = qmodel([x])[0]
+    qmodel.keep_values = False
+    plan, two, one = _split_vs_one_stream(qmodel, x)
+    assert plan.fused == 1
+    for _ in range(3):
+        np.testing.assert_array_equal(qmodel([x])[0], eager)
+    np.testing.assert_array_equal(two, eager)
+    np.testing.assert_array_equal(one, eager)
+
+
+def test_plan_restores_stream_after_error():
+    """An exception inside a split half leaves the library on stream 0 and joined."""
+    from numpy_quant import _lib
+    from numpy_quant.plan import Streams
+    s = Streams(True)
+
+    def boom(s_idx, i0, nb):
+        if s_idx == 1:
+            raise RuntimeError("boom")
+
+    with pytest.raises(RuntimeError):
+        s.halves(4, boom)
+    s.join()
+    import ctypes
+    cur, base = ctypes.c_void_p(), ctypes.c_void_p()
+    _lib.call("nqk_stream", ctypes.byref(cur))
+    _lib.call("nqk_set_stream", 0)
+    _lib.call("nqk_stream", ctypes.byref(base))
+    assert cur.value == base.value
