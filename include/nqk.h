@@ -215,6 +215,8 @@ typedef struct nqk_epilogue {
   const float* resid;                   /* residual [M][N] (EPI_RESID)                  */
   float div, add1, mul2;                /* Div constant (8 / sqrt 2), GELU +1 and *0.5  */
   int32_t b_packed;                     /* 1: bt is an nqk_pack_b image; 2: nqk_pack_b4  */
+  const int32_t* colterm;               /* optional: col[n] * zpa as int32 (the persistent */
+                                        /* projection GEMM needs it; NULL: not used)     */
 } nqk_epilogue;
 /* int8 MFMA GEMM C = A . Bt^T (layouts as nqk_qgemm_i8) with a fused epilogue:
  *   QKV    model.py MatMul -> Add(bias) -> Reshape -> Transpose -> quantize, 3 groups
@@ -235,6 +237,10 @@ int nqk_pack_b4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t ld
 int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, int64_t M, int64_t N, int64_t K,
                     int64_t lda, int64_t ldb, const int64_t* bmap, int64_t a_mat_stride, int64_t b_mat_stride,
                     const nqk_epilogue* params);
+/* Which kernel the last nqk_qgemm_fused call launched (tests / diagnostics): 0 small tiles
+ * (k_qgemm_epi), 1 128x256 tiles (k_qgemm_big), 2 ping-pong 256x256 (k_qgemm_pp), 3 the
+ * persistent projection GEMM with the epilogue overlapped (k_proj); -1 none yet. */
+int nqk_qgemm_last_kernel(void);
 /* LayerNormalization (model.py:134-152) fused with the consumer MatMul's quantize */
 int nqk_ln_quant(const float* x, const float* gamma, const float* beta, int8_t* out, int64_t rows, int64_t cols,
                  float eps, float scale, int64_t zp, int bit_width);

@@ -78,6 +78,7 @@ struct Epi {
   float lof, hif;            // lo, hi as f32
   float g_rel, g_abs;        // GELU filter error terms, in units of t
   int b_packed;              // Bt is the tile-packed image of nqk_pack_b
+  const int32_t* colterm;    // int32 col * zpa (k_proj), or null
 };
 
 enum { EPI_QKV = 0, EPI_SCORES = 1, EPI_PV = 2, EPI_RESID = 3, EPI_GELU = 4, EPI_NULL = 5 };
@@ -900,6 +901,476 @@ k_qgemm_pp(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, i
   proj_epilogue<EPI, I32, F32X>(lds, acc, e, m0 + grp * 128, n0 + wn * 64, M, N, wave, lane);
 }
 
+// ---------------------------------------------------------------------------------------
+// k_proj: persistent projection GEMM with 256 x 256 tiles, A [M][K] int8 x a tile-packed
+// constant weight image (nqk_pack_b / nqk_pack_b4), K = 64 NK (NK = 12: K 768, NK = 48:
+// K 3072), M % 256 == 0, N % 256 == 0.  One 512-thread workgroup per CU walks its tiles in
+// order (every XCD owns a contiguous band of tile ids: the tiles in flight on one XCD
+// share A row panels in its L2).  8 waves as 2 (M) x 4 (N), each owning 128 x 64 outputs
+// (4 x 2 tiles of v_mfma_i32_32x32x32_i8, 128 accumulators).
+//
+// What bounds these GEMMs on MI355X (measured, tools/micro and DESIGN.md): the LDS-DMA
+// stream from L2 delivers ~24 B per clock per CU, and on one SIMD the matrix pipe and the
+// vector pipe do not overlap across waves.  So the tile is as large as the registers
+// allow (256 x 256: 32 KiB staged per 1024 MFMA cycles, half the bytes per MFMA of the
+// 128 x 256 kernel), the k loop keeps MFMAs issuing (the next k-step's fragment reads
+// and stage publication sit between the two MFMA halves of a step), and the epilogue
+// runs after the k loop with the next tile's first two stages already in flight.
+// Epilogue values leave straight from the MFMA layout: QKV / GELU tiles are computed
+// transposed (lane = row, 4 consecutive columns per register group: 4-byte stores of 4
+// int8 values), RESID tiles not (lane = column: 2 rows x 128 B of f32 per store).  The
+// column constants (int32 zero-point column terms, biases) and the residual arrive by
+// LDS-DMA / buffer LDS-DMA and every VMEM operation is counted by the compile-time vmcnt
+// waits (an ordinary VGPR load in the loop would make the compiler drain the LDS-DMA
+// queue at its first use).
+// LDS: ring of P2_DEPTH stages (4 x 32 KiB int8, 4 x 24 KiB int4 weights; EPI_RESID 3
+// stages) | column constants 2 KiB | EPI_RESID: residual, 8 waves x 2 slots x 2 KiB =
+// 32 KiB.  The ring depth is what the k loop's speed comes from: L2 delivers ~57 B per
+// clock per CU into LDS (tools/micro/l2bw.hip) only with ~100 KiB in flight per CU; a
+// 3-deep ring (one stage of lead) left the loop at ~24 B per clock.
+constexpr int p2_depth(int epi) { return epi == EPI_RESID ? 3 : 4; }
+constexpr int p2_stage(bool b4) { return 256 * GBK + GBN * (b4 ? GBK / 2 : GBK); }
+constexpr int p2_colp(int epi, bool b4) { return p2_depth(epi) * p2_stage(b4); }
+constexpr int p2_res(int epi, bool b4) { return p2_colp(epi, b4) + 2048; }
+constexpr int p2_lds(int epi, bool b4) { return p2_res(epi, b4) + (epi == EPI_RESID ? 8 * 2 * 2048 : 0); }
+
+template <int I>
+using ic = std::integral_constant<int, I>;
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(ic<B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// LDS reads the compiler cannot see: a visible read of LDS-DMA'd bytes may get an
+// s_waitcnt vmcnt(0) (it cannot prove the read misses the DMA in flight), which would
+// drain the operand ring; the caller waits lgkmcnt
+__device__ __forceinline__ int lds_read4(const void* p) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)p));
+  return v;
+}
+__device__ __forceinline__ v4i lds_read16(const void* p) {
+  v4i v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)p));
+  return v;
+}
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// 16-byte buffer LDS-DMA (a device function: used from a kernel's lambdas the builtin
+// made the host pass drop the kernel's launch stub)
+__device__ __forceinline__ void buf_lds16(rsrc_t r, void* l, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)l, 16, voff, soff, 0, 0);
+}
+
+#ifndef NQK_PJ_DIAG
+#define NQK_PJ_DIAG 0  // diagnostic builds only: 1 = no epilogue stores, 2 = trivial epilogue math,
+                      // 4 = no operand loads, 8 = no k-loop barriers, 16 = no fragment reads,
+                      // 32 = no epilogue (results garbage)
+#endif
+
+// QKV / GELU epilogue of NG register groups of a transposed tile: group x = accumulators
+// a[x][0..3] = 4 consecutive columns (column terms ct[x], biases bs[x]) of this lane's
+// row; per element the operations of epi_row4 with the F32X rounding filters.  The fast
+// path of all groups is one basic block (independent chains), then one wave-wide check
+// sends the elements the filter could not decide through the exact chain.  Returns the
+// 4 int8 results of each group packed in a dword.
+template <int EPI, int ASH, int NG>
+__device__ __forceinline__ void p2_quant(const Epi& e, const int (&a)[NG][4], const v4i (&ct)[NG],
+                                         const v4i (&bs)[NG], float sacc, float rsf, float zpf, float s_out,
+                                         double rs_out, double zp, uint32_t (&packed)[NG]) {
+  constexpr int E = 4 * NG;
+  int q[E];
+  float hv[E];
+  bool slow[E];
+  bool any = false;
+#pragma unroll
+  for (int x = 0; x < E; ++x) {
+    const int v = (a[x >> 2][x & 3] >> ASH) - ct[x >> 2][x & 3];
+    const float h = __int_as_float(bs[x >> 2][x & 3]) + (float)v * sacc;  // the f64 dequantize, exactly (F32X)
+    hv[x] = h;
+    if constexpr ((NQK_PJ_DIAG & 2) != 0) {
+      q[x] = v;
+      slow[x] = false;
+      continue;
+    }
+    float tf, thr;
+    if constexpr (EPI == EPI_GELU) {
+      tf = gelu_fast(h) * rsf;
+      thr = __builtin_fmaf(__builtin_fabsf(h), e.g_rel, e.g_abs);
+    } else {
+      tf = h * rsf;
+      thr = __builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, 0x1p-126f);
+    }
+    const float r = __builtin_rintf(tf);
+    const float room = 0.5f - __builtin_fabsf(tf - r);
+    slow[x] = !(room > thr);
+    any |= slow[x];
+    q[x] = (int)__builtin_amdgcn_fmed3f(r + zpf, e.lof, e.hif);
+  }
+  if (__builtin_expect(__any(any), 0)) {
+#pragma unroll
+    for (int x = 0; x < E; ++x) {
+      if (__any(slow[x])) {
+        if (slow[x]) {
+          float y = hv[x];
+          if constexpr (EPI == EPI_GELU) {
+            const float aa = ref_erf(div_rc_u(y, e.div, e.rdiv)) + e.add1;
+            y = (y * aa) * e.mul2;
+          }
+          q[x] = quant_zp_u(y, s_out, rs_out, zp, e.lo, e.hi);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+    packed[g] = ((uint32_t)q[4 * g] & 0xffu) | (((uint32_t)q[4 * g + 1] & 0xffu) << 8) |
+                (((uint32_t)q[4 * g + 2] & 0xffu) << 16) | ((uint32_t)q[4 * g + 3] << 24);
+}
+
+template <int EPI, bool F32X, int NK, bool B4>
+__global__ void __launch_bounds__(512, 1)
+k_proj(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
+       Epi e) {
+  constexpr bool RESID = EPI == EPI_RESID;
+  constexpr bool TRANS = !RESID;               // lane = row (QKV / GELU) or lane = column (RESID)
+  constexpr int BROW = B4 ? GBK / 2 : GBK;     // bytes of one B row per k-step
+  constexpr int BPW = GBN * BROW / 1024 / 8;   // B pieces per wave per stage (2 / 1)
+  constexpr int PW = 2 + BPW;                  // ring pieces per wave per stage
+  constexpr int STG = 256 * GBK + GBN * BROW;
+  constexpr int RD = p2_depth(EPI);
+  static_assert(NK % RD == 0 && NK >= 2 * RD, "k_proj: NK a multiple of the ring depth");
+  static_assert(p2_lds(EPI, B4) <= 160 * 1024, "k_proj: LDS");
+  // VMEM operations of one epilogue: QKV / GELU 32 stores; RESID 15 x 8 residual loads +
+  // 16 x 8 stores (the counter never holds more than 63)
+  constexpr int EOPS = RESID ? 248 : 32;
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int r32 = lane & 31, half = lane >> 5;
+
+  // this workgroup's tiles: XCD label x = blockIdx % X owns the band [lo, hi) of tile ids
+  // and its workgroups take every nx-th tile from lo + jx (X = 8, fewer on a small grid)
+  const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X, jx = blockIdx.x / X;
+  const int nx = (G - x + X - 1) / X;
+  const int lo = (int)((int64_t)ntiles * x / X), hi = (int)((int64_t)ntiles * (x + 1) / X);
+  const int first = lo + jx;
+  if (first >= hi) return;
+  const int cnt = (hi - first + nx - 1) / nx;
+  const int64_t bstride = (int64_t)NK * GBN * BROW;
+
+  // operands by buffer LDS-DMA: per lane one 32-bit offset each (A: the row and swizzled
+  // 16-byte chunk this lane fetches; B: its 16 bytes of a 1 KiB piece), the tile and the
+  // k-step in scalar offsets
+  const rsrc_t r_a = make_rsrc(A, (uint32_t)((uint64_t)M * lda));
+  const rsrc_t r_b = make_rsrc(Bp, (uint32_t)((uint64_t)tiles_n * bstride));
+  const uint32_t va = [&] {
+    const int row0 = wave * 32 + (lane >> 2), pos = lane & 3;
+    return (uint32_t)(row0 * lda + ((pos ^ ((row0 >> 2) & 3)) << 4));
+  }();
+  const uint32_t vb = (uint32_t)(wave * BPW * 1024 + lane * 16);
+  struct Src { uint32_t sa, sb; int r0, tn; };  // r0: the tile's first row
+  auto src_of = [&](int tile) __attribute__((always_inline)) {
+    Src s;
+    const int tm = tile / tiles_n;
+    s.tn = tile - tm * tiles_n;
+    // a ragged last tile row is computed as rows M - 256 .. M - 1 (QKV / GELU only, host:
+    // the rows it shares with the tile above are written twice with the same bytes)
+    s.r0 = tm * 256 < M - 256 ? tm * 256 : M - 256;
+    s.sa = (uint32_t)s.r0 * (uint32_t)lda;
+    s.sb = (uint32_t)s.tn * (uint32_t)bstride;
+    return s;
+  };
+  auto issue_stage = [&](const Src& s, auto KT, int slot) __attribute__((always_inline)) {
+    constexpr int kt = decltype(KT)::value;
+    if constexpr ((NQK_PJ_DIAG & 4) != 0) return;  // diagnostic: no operand loads
+    int8_t* st = lds + slot * STG;
+    // rows row0 and row0 + 16 (same swizzle: (row >> 2) & 3 repeats every 16 rows)
+    buf_lds16(r_a, st + (2 * wave) * 1024, va, s.sa + kt * GBK);
+    buf_lds16(r_a, st + (2 * wave + 1) * 1024, va, s.sa + 16u * (uint32_t)lda + kt * GBK);
+#pragma unroll
+    for (int p = 0; p < BPW; ++p)
+      buf_lds16(r_b, st + 256 * GBK + (wave * BPW + p) * 1024, vb, s.sb + (uint32_t)(kt * GBN * BROW + p * 1024));
+  };
+  int8_t* const colp = lds + p2_colp(EPI, B4);
+  auto issue_colp = [&](int tn) __attribute__((always_inline)) {  // waves 0 (ct) and 1 (bias)
+    const int n0 = tn * GBN;
+    if (wave == 0) {
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(reinterpret_cast<const int8_t*>(e.colterm + n0) + lane * 16),
+                                       (lds_ptr_t)colp, 16, 0, 0);
+    } else if (wave == 1 && e.bias != nullptr) {
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(reinterpret_cast<const int8_t*>(e.bias + n0) + lane * 16),
+                                       (lds_ptr_t)(colp + 1024), 16, 0, 0);
+    }
+  };
+  const rsrc_t r_res = make_rsrc(e.resid, RESID ? (uint32_t)((uint64_t)M * N * 4) : 0u);
+  // RESID chunk c (0..15): MFMA tile (i, j) = (c >> 2, (c >> 1) & 1), registers 8 (c & 1) ..
+  // + 7 = rows rb + 8 (el >> 2) + (el & 3) of column n
+  auto res_slot = [&](int c) __attribute__((always_inline)) { return lds + p2_res(EPI, B4) + (wave * 2 + (c & 1)) * 2048; };
+  auto issue_res = [&](const Src& s, int c) __attribute__((always_inline)) {
+    if constexpr (RESID) {
+      const int i = c >> 2, j = (c >> 1) & 1, hs = c & 1;
+      const uint32_t rb = s.r0 + wm * 128 + i * 32 + 16 * hs + 4 * half;
+      const uint32_t n = s.tn * GBN + wn * 64 + j * 32 + r32;
+      const uint32_t o = (rb * (uint32_t)N + n) * 4u;
+#pragma unroll
+      for (int el = 0; el < 8; ++el)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r_res, (lds_ptr_t)(res_slot(c) + el * 256), 4, o,
+                                                 (8 * (el >> 2) + (el & 3)) * N * 4, 0, 0);
+    }
+  };
+
+  v16i acc[4][2];
+  v4i f0a[4], f0b[2], f1a[4], f1b[2];  // the two k halves' fragments
+  // fragment q of k half s from ring slot `slot`: q 0..3 the A rows of M-subtile q, 4..5
+  // the B rows of N-subtile q - 4
+  auto read_frag = [&](int slot, int s, int q, v4i (&fa)[4], v4i (&fb)[2]) __attribute__((always_inline)) {
+    const int8_t* sa = lds + slot * STG;
+    const int8_t* sb = sa + 256 * GBK;
+    if constexpr ((NQK_PJ_DIAG & 16) != 0) return;  // diagnostic: no fragment reads
+    if (q < 4) {
+      fa[q] = *reinterpret_cast<const v4i*>(sa + swz64(wm * 128 + q * 32 + r32, 2 * half + s));
+    } else {
+      const int j = q - 4, row = wn * 64 + j * 32 + r32, c = 2 * half + s;
+      if constexpr (B4) {
+        // nibbles (inline asm read: see lds_read4); unpacked after an lgkmcnt wait
+        uint2 w;
+        asm volatile("ds_read_b64 %0, %1" : "=v"(w)
+                     : "v"((uint32_t)(uintptr_t)(lds_ptr_t)(sb + row * 32 + ((c ^ ((row >> 3) & 3)) << 3))));
+        fb[j] = v4i{(int)w.x, (int)w.y, 0, 0};
+      } else {
+        fb[j] = *reinterpret_cast<const v4i*>(sb + swz64(row, c));
+      }
+    }
+  };
+  auto read_frags = [&](int slot, int s, v4i (&fa)[4], v4i (&fb)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) read_frag(slot, s, q, fa, fb);
+  };
+  auto unpack = [&](v4i (&fb)[2]) __attribute__((always_inline)) {
+    if constexpr (B4) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t wx = (uint32_t)fb[j][0], wy = (uint32_t)fb[j][1];
+        fb[j] = v4i{(int)((wx << 4) & 0xF0F0F0F0u), (int)(wx & 0xF0F0F0F0u), (int)((wy << 4) & 0xF0F0F0F0u),
+                    (int)(wy & 0xF0F0F0F0u)};
+      }
+    }
+  };
+  // the 8 MFMAs of one k half, with fn(q) issued after MFMA q (LDS reads and LDS-DMA
+  // between MFMAs: one wave's in-order issue keeps the matrix pipe fed while they go out)
+  auto mfmas = [&](const v4i (&fa)[4], const v4i (&fb)[2], auto&& fn) __attribute__((always_inline)) {
+    static_for<0, 8>([&](auto Q) __attribute__((always_inline)) {
+      constexpr int q = decltype(Q)::value, i = q >> 1, j = q & 1;
+      if constexpr (TRANS) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      else acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      fn(Q);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
+  // ---- the epilogue of tile s (accumulators in acc)
+  auto epilogue = [&](const Src& s) __attribute__((always_inline)) {
+    const int r0 = s.r0, n0 = s.tn * GBN;
+    if constexpr ((NQK_PJ_DIAG & 32) != 0) {  // diagnostic: no epilogue
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[i][j][0]));
+      return;
+    }
+    if constexpr (RESID) {
+      int ct[2];
+      float bias[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cl = wn * 64 + j * 32 + r32;
+        ct[j] = lds_read4(colp + cl * 4);
+        bias[j] = e.bias ? __int_as_float(lds_read4(colp + 1024 + cl * 4)) : 0.0f;
+      }
+      const rsrc_t out = make_rsrc(e.out[0], (uint32_t)((uint64_t)M * N * 4));
+      static_for<0, 16>([&](auto CI) __attribute__((always_inline)) {
+        constexpr int c = decltype(CI)::value;
+        constexpr int i = c >> 2, j = (c >> 1) & 1, hs = c & 1;
+        // residual of chunk c landed (issued before the previous chunk's stores; chunk 0:
+        // at the last k-step, before the RD - 1 prefetched stages)
+        if constexpr (c == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((p2_depth(EPI) - 1) * PW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        float res[8];
+#pragma unroll
+        for (int el = 0; el < 8; ++el) res[el] = __int_as_float(lds_read4(res_slot(c) + el * 256 + lane * 4));
+        lgkm_wait();
+        if constexpr (c + 1 < 16) issue_res(s, c + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t rb = r0 + wm * 128 + i * 32 + 16 * hs + 4 * half;
+        const uint32_t o = (rb * (uint32_t)N + (uint32_t)(n0 + wn * 64 + j * 32 + r32)) * 4u;
+        const int ctj = ct[j];
+        float y[8];
+#pragma unroll
+        for (int el = 0; el < 8; ++el) {
+          const int v = (acc[i][j][8 * hs + el] >> (B4 ? 4 : 0)) - ctj;
+          const float d = F32X ? (float)v * e.s_acc[0] : (float)((double)v * (double)e.s_acc[0]);
+          y[el] = (bias[j] + d) + res[el];
+        }
+#pragma unroll
+        for (int el = 0; el < 8; ++el)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y[el]), out, o, (8 * (el >> 2) + (el & 3)) * N * 4, 0);
+      });
+    } else {
+      // transposed tile: lane = row m of M-subtile i, group (j, g) = 4 consecutive columns
+      // n_local = wn * 64 + j * 32 + 8 g + 4 half .. + 3
+      const int cw = n0 + wn * 64;  // the wave's 64 columns: one head, one column group (host)
+      int g3 = 0;
+      uint32_t rowoff[4];
+      if constexpr (EPI == EPI_QKV) {
+        g3 = cw / e.group_cols;
+        g3 = g3 > 2 ? 2 : g3;
+        const int hh = (cw - g3 * e.group_cols) / e.hdim;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = r0 + wm * 128 + i * 32 + r32;
+          const int img = m / e.tokens, t = m - img * e.tokens;
+          rowoff[i] = (uint32_t)(((img * e.heads + hh) * e.tokens + t) * e.hdim) + 4 * half;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rowoff[i] = (uint32_t)(r0 + wm * 128 + i * 32 + r32) * (uint32_t)N + cw + 4 * half;
+      }
+      const float sacc = g3 == 0 ? e.s_acc[0] : (g3 == 1 ? e.s_acc[1] : e.s_acc[2]);
+      const float rsf = g3 == 0 ? e.rsf[0] : (g3 == 1 ? e.rsf[1] : e.rsf[2]);
+      const float zpf = g3 == 0 ? e.zpf[0] : (g3 == 1 ? e.zpf[1] : e.zpf[2]);
+      const float s_out = g3 == 0 ? e.s_out[0] : (g3 == 1 ? e.s_out[1] : e.s_out[2]);
+      const double rs_out = g3 == 0 ? e.rs_out[0] : (g3 == 1 ? e.rs_out[1] : e.rs_out[2]);
+      const double zp = g3 == 0 ? e.zp_out[0] : (g3 == 1 ? e.zp_out[1] : e.zp_out[2]);
+      void* op = g3 == 0 ? e.out[0] : (g3 == 1 ? e.out[1] : e.out[2]);
+      const rsrc_t out = make_rsrc(op, (uint32_t)(EPI == EPI_QKV ? (uint64_t)M * e.group_cols : (uint64_t)M * N));
+      // batches of NG register groups (QKV: a whole MFMA tile, 16 values; GELU, whose
+      // fast path holds more temporaries: half a tile), j-major: the column constants of
+      // the lane's 4 column groups of N-subtile j are read at its first batch
+      constexpr int NG = EPI == EPI_GELU ? 2 : 4, NB = 32 / NG;
+      v4i ct[4], bs[4];
+      static_for<0, NB>([&](auto BI) __attribute__((always_inline)) {
+        constexpr int b = decltype(BI)::value, j = b / (NB / 2), i = (b % (NB / 2)) / (4 / NG),
+                      g0 = (b % (4 / NG)) * NG;
+        if constexpr (b % (NB / 2) == 0) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int cl = wn * 64 + j * 32 + 8 * g + 4 * half;
+            ct[g] = lds_read16(colp + cl * 4);
+            bs[g] = e.bias ? lds_read16(colp + 1024 + cl * 4) : v4i{0, 0, 0, 0};
+          }
+          lgkm_wait();
+        }
+        int a[NG][4];
+        v4i cg[NG], bg[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          cg[g] = ct[g0 + g];
+          bg[g] = bs[g0 + g];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) a[g][k] = acc[i][j][4 * (g0 + g) + k];
+        }
+        uint32_t packed[NG];
+        p2_quant<EPI, B4 ? 4 : 0, NG>(e, a, cg, bg, sacc, rsf, zpf, s_out, rs_out, zp, packed);
+        if constexpr ((NQK_PJ_DIAG & 1) != 0) {
+          uint32_t t = 0;
+#pragma unroll
+          for (int g = 0; g < NG; ++g) t ^= packed[g];
+          asm volatile("" ::"v"(t));
+        } else {
+#pragma unroll
+          for (int g = 0; g < NG; ++g)
+            __builtin_amdgcn_raw_buffer_store_b32(packed[g], out, rowoff[i] + j * 32 + 8 * (g0 + g), 0, 0);
+        }
+      });
+    }
+  };
+
+  // ---- the persistent loop.  Stages PF = RD - 1 ahead: the stage read at step kt + PF
+  // goes into the slot step kt - 1 read (every wave's reads of it retired before the
+  // barrier in the middle of step kt - 1)
+  constexpr int PF = RD - 1;
+  auto cap = [](int n) constexpr { return n > 63 ? 63 : n; };
+  Src cur = src_of(first);
+  static_for<0, PF>([&](auto S) __attribute__((always_inline)) { issue_stage(cur, S, decltype(S)::value); });
+  for (int it = 0; it < cnt; ++it) {
+    const Src nxt = src_of(first + (it + 1 < cnt ? it + 1 : it) * nx);
+    // stage 0 of this tile landed (younger: stages 1 .. PF - 1 and the previous
+    // epilogue's operations)
+    if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PF - 1) * PW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(cap((PF - 1) * PW + EOPS)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags(0, 0, f0a, f0b);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+    static_for<0, NK>([&](auto KT) __attribute__((always_inline)) {
+      constexpr int kt = decltype(KT)::value;
+      // first k half: F0 (read one barrier ago) in the MFMAs; between them the second
+      // half's fragments (slot kt % RD), the column constants (step 0), the residual of
+      // the epilogue's first chunk (last step) and the ring stage kt + PF
+      if constexpr (B4) {
+        lgkm_wait();
+        unpack(f0b);
+      }
+      mfmas(f0a, f0b, [&](auto Q) __attribute__((always_inline)) {
+        constexpr int q = decltype(Q)::value;
+        if constexpr (q < 6) read_frag(kt % RD, 1, q, f1a, f1b);
+        if constexpr (q == 6) {
+          if constexpr (kt == 0) issue_colp(cur.tn);
+          if constexpr (RESID && kt == NK - 1) issue_res(cur, 0);
+          if constexpr (kt + PF < NK) issue_stage(cur, ic<kt + PF>{}, (kt + PF) % RD);
+        }
+      });
+      if constexpr (kt + 1 < NK) {
+        // stage kt + 1 landed (younger: the stages kt + 2 .. kt + PF issued; for the
+        // stages prefetched before the previous epilogue also its operations) and this
+        // step's fragment reads retired; then the barrier publishes stage kt + 1
+        constexpr int last = kt + PF < NK ? kt + PF : NK - 1;
+        constexpr int younger = (last >= kt + 2 ? last - kt - 1 : 0) * PW;
+        if (kt + 1 <= PF - 1 && it > 0)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(cap(younger + EOPS)) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(younger) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr ((NQK_PJ_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();  // diagnostic: none
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (B4) {
+        lgkm_wait();
+      }
+      if constexpr (B4) unpack(f1b);
+      // second k half, the next step's first-half fragments read between its MFMAs
+      mfmas(f1a, f1b, [&](auto Q) __attribute__((always_inline)) {
+        constexpr int q = decltype(Q)::value;
+        if constexpr (kt + 1 < NK && q < 6) read_frag((kt + 1) % RD, 0, q, f0a, f0b);
+      });
+    });
+    // the next tile's first PF stages fly during the epilogue (slot s was last read at
+    // step NK - RD + s <= NK - 2, whose middle barrier every wave has passed)
+    static_for<0, PF>([&](auto S) __attribute__((always_inline)) { issue_stage(nxt, S, decltype(S)::value); });
+    __builtin_amdgcn_sched_barrier(0);
+    epilogue(cur);
+    cur = nxt;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Tile-packed image of a constant weight operand Bt [N][K] for k_qgemm_big: for column
 // panel tn (256 rows, zero padded past N) and k-step kt (64 bytes), one 16 KiB block whose
 // byte row*64 + pos*16 + b holds Bt[tn*256 + row][kt*64 + (pos ^ ((row >> 2) & 3))*16 + b]:
@@ -1171,6 +1642,28 @@ static void launch_big(bool pp, const int8_t* a, const int8_t* bt, int64_t M, in
   }
 }
 
+static int g_last_gemm = -1;  // nqk_qgemm_last_kernel: 0 small tiles, 1 big tile, 2 ping-pong, 3 persistent
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int EPI, bool F32X, int NK, bool B4>
+static void launch_proj(const int8_t* a, const int8_t* bp, int64_t M, int64_t N, int64_t lda, const Epi& e) {
+  const int tn = (int)(N / GBN), nt = (int)((M + 255) / 256) * tn;
+  const int grid = nt < num_cus() ? nt : num_cus();
+  const size_t shm = p2_lds(EPI, B4);
+  hipLaunchKernelGGL((k_proj<EPI, F32X, NK, B4>), dim3(grid), dim3(512), shm, stream(), a, bp, (int)M, (int)N, (int)lda,
+                     tn, nt, e);
+}
+
 static Epi make_epi(const nqk_epilogue* p) {
   Epi e{};
   e.zp_flags = p->zp_flags;
@@ -1213,6 +1706,7 @@ static Epi make_epi(const nqk_epilogue* p) {
   e.g_rel = (float)((double)GELU_REL * 1.27 * ars);
   e.g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
   e.b_packed = p->b_packed;
+  e.colterm = p->colterm;
   e.lof = (float)e.lo;
   e.hif = (float)e.hi;
   return e;
@@ -1284,6 +1778,36 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     const bool f32x = i32 && (epi == EPI_QKV || (epi == EPI_GELU && e.gelu_filter)) && zp_small &&
                       16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
     const bool use_pp = pp && !params->b_packed;
+    // the persistent 256 x 256 kernel where it takes the shape (QKV / GELU; the residual
+    // epilogues only with NQK_PROJ_RESID=1: their f32 residual read + output write is HBM
+    // traffic the one-tile-per-workgroup kernel overlaps better);
+    // NQK_NO_PROJ=1 keeps the one-tile-per-workgroup kernel
+    const bool f32x_r = i32 && epi == EPI_RESID && 16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
+    const bool proj_shape = params->b_packed && i32 && params->colterm != nullptr && M >= 256 && (M % 256 == 0 || epi != EPI_RESID) && N % GBN == 0 &&
+                            (K == 768 || K == 3072) && (double)M * N * 4.0 < 4294967295.0 && (double)M * lda < 4294967295.0 &&
+                            !getenv("NQK_NO_PROJ") &&
+                            ((epi == EPI_RESID && !(params->b_packed == 2 && K == 768) && getenv("NQK_PROJ_RESID")) ||
+                             (f32x && K == 768 &&
+                              (epi == EPI_GELU ||
+                               (epi == EPI_QKV && params->tokens >= 64 && params->hdim == 64 && params->group_cols % 128 == 0 &&
+                                (double)M * params->heads * params->hdim < 2147483647.0))));
+    if (proj_shape) {
+      const bool b4 = params->b_packed == 2;
+      const int key = epi * 8 + (b4 ? 4 : 0) + (K == 3072 ? 2 : 0) + (f32x || f32x_r ? 1 : 0);
+      switch (key) {
+#define LP(E, B, NKV, X) case E * 8 + (B ? 4 : 0) + (NKV == 48 ? 2 : 0) + (X ? 1 : 0): \
+        launch_proj<E, X, NKV, B>(a, bt, M, N, lda, e); break;
+        LP(EPI_QKV, false, 12, true) LP(EPI_QKV, true, 12, true)
+        LP(EPI_GELU, false, 12, true) LP(EPI_GELU, true, 12, true)
+        LP(EPI_RESID, false, 12, true) LP(EPI_RESID, false, 12, false)
+        LP(EPI_RESID, false, 48, false) LP(EPI_RESID, true, 48, false)
+        LP(EPI_RESID, false, 48, true) LP(EPI_RESID, true, 48, true)
+#undef LP
+        default: return fail("nqk_qgemm_fused: no persistent kernel for this case");
+      }
+      g_last_gemm = 3;
+      return launch_status("nqk_qgemm_fused(proj)");
+    }
     switch (epi * 3 + (f32x ? 2 : (i32 ? 1 : 0))) {
 #define LB(E) \
       case E * 3 + 0: launch_big<E, false, false>(use_pp, a, bt, M, N, K, lda, ldb, e); break; \
@@ -1294,8 +1818,10 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
       case EPI_GELU * 3 + 2: launch_big<EPI_GELU, true, true>(use_pp, a, bt, M, N, K, lda, ldb, e); break;
       default: return fail("nqk_qgemm_fused: no big-tile kernel for this epilogue");
     }
+    g_last_gemm = use_pp ? 2 : 1;
     return launch_status("nqk_qgemm_fused(big)");
   }
+  g_last_gemm = 0;
   const int tiles_m = (int)((M + FBM - 1) / FBM), tiles_n = (int)((N + FBN - 1) / FBN);
   const BatchMap m = batch_map(bmap);
   const dim3 grid(tiles_m * tiles_n, 1, (unsigned)batch);
@@ -1310,6 +1836,8 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   }
   return launch_status("nqk_qgemm_fused");
 }
+
+extern "C" int nqk_qgemm_last_kernel(void) { return g_last_gemm; }
 
 extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* beta, int8_t* out, int64_t rows,
                             int64_t cols, float eps, float scale, int64_t zp, int bit_width) {

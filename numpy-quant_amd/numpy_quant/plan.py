@@ -543,6 +543,10 @@ class FusedLayer:
         # max |column sum| of each weight: lets the GEMM epilogues prove f32 exactness
         self.cmax = {k: _absmax(c) for k, c in (("qkv", self.col_qkv), ("o", self.col_o), ("1", self.col_1),
                                                  ("2", self.col_2))}
+        # int32 zero-point column terms col * zp_a of each GEMM (the persistent GEMM's
+        # per-column constant; None where they do not fit int32)
+        self.ct = {k: _colterm(c, _zp(p)) for k, c, p in (("qkv", self.col_qkv, self.p_ln1), ("o", self.col_o, self.p_ctx),
+                                                          ("1", self.col_1, self.p_ln2), ("2", self.col_2, self.p_h))}
         if self.D != m.heads * m.hdim or self.bt_o.shape != (self.D, self.D) or self.bt_2.shape != (self.D, self.F):
             raise NoMatch("layer dimensions")
         # the one-kernel attention covers head size 64, <= 224 tokens and zero points for
@@ -639,7 +643,7 @@ class FusedLayer:
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D, col=self.col_qkv.ptr,
-                      col_absmax=self.cmax["qkv"],
+                      col_absmax=self.cmax["qkv"], colterm=_ptr(self.ct["qkv"]),
                       s_acc=[_f32(s_a * np.float32(self.s_w[r])) for r in "qkv"],
                       s_out=[_f32(self.p_head[r].scale) for r in "qkv"],
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
@@ -663,6 +667,7 @@ class FusedLayer:
             self._attention_unfused(w, nb, T, Tp, H, Dh, D)  # whole batch only (i0 == 0)
         # 7) output projection + bias + residual
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr, col_absmax=self.cmax["o"],
+                      colterm=_ptr(self.ct["o"]),
                       s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
                       resid=x.ptr, out=[x1.ptr])
         _gemm(EPI_RESID, ctx, self._b(e, "o", self.bt_o), 1, Mrows, D, D, D, D, None, 0, 0, e)
@@ -670,12 +675,14 @@ class FusedLayer:
         _ln_quant(x1, self.g2, self.be2, ln2q, Mrows, D, self.eps2, self.p_ln2, bw)
         # 9) FFN up + bias + GELU + quantize
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr, col_absmax=self.cmax["1"],
+                      colterm=_ptr(self.ct["1"]),
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
                       s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[hh.ptr],
                       div=m.gelu_div, add1=m.gelu_add, mul2=m.gelu_mul)
         _gemm(EPI_GELU, ln2q, self._b(e, "1", self.bt_1), 1, Mrows, F, D, D, D, None, 0, 0, e)
         # 10) FFN down + bias + residual
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr, col_absmax=self.cmax["2"],
+                      colterm=_ptr(self.ct["2"]),
                       s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
                       resid=x1.ptr, out=[x2.ptr])
         _gemm(EPI_RESID, hh, self._b(e, "2", self.bt_2), 1, Mrows, D, F, F, F, None, 0, 0, e)
@@ -698,6 +705,14 @@ def _pack_b(bt, bit_width=8):
     return out, 1
 
 
+def _colterm(col, zpa):
+    """col * zpa as an int32 device array, or None when a term leaves int32."""
+    c = col.to_host().astype(np.int64) * int(zpa)
+    if c.size and (c.min() < -2 ** 31 or c.max() >= 2 ** 31):
+        return None
+    return DeviceArray.from_host(c.astype(np.int32))
+
+
 def _absmax(col) -> int:
     """max |column sum| (int32-clamped; 0 would mean unknown to the kernel, so >= 1)."""
     v = int(np.abs(col.to_host()).max()) if col.size else 1
@@ -709,6 +724,10 @@ def _ln_quant(x, g, b, out, rows, cols, eps, p, bw):
     _lib.call("nqk_ln_quant", x.vp, g.vp, b.vp, out.vp, rows, cols, eps, _f32(p.scale), _zp(p), bw)
     if t0 is not None:
         KM.TIMER.end("ln_quant", t0, (0, rows * cols * 5 + 2 * cols * 4))
+
+
+def _ptr(arr):
+    return None if arr is None else arr.ptr
 
 
 def _cat0(arrs):

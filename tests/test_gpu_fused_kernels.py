@@ -206,3 +206,78 @@ def test_int4_packed_weights_equal_int8_path(epi_name, M, N, K, monkeypatch):
         outs.append([b.to_host() for b in bufs])
     for x, y in zip(outs[0], outs[1]):
         np.testing.assert_array_equal(x, y)
+
+
+def _last_kernel():
+    from numpy_quant import _lib
+    return _lib.load().nqk_qgemm_last_kernel()
+
+
+@pytest.mark.parametrize("epi_name,M,N,K,bw", [
+    ("qkv", 256 * 197, 2304, 768, 8), ("qkv", 256 * 197, 2304, 768, 4),
+    ("gelu", 128 * 50, 3072, 768, 8), ("gelu", 128 * 50, 3072, 768, 4), ("gelu", 512, 3072, 768, 8),
+    ("resid", 128 * 200, 768, 768, 8), ("resid", 128 * 200, 768, 3072, 8), ("resid", 128 * 200, 768, 3072, 4),
+    ("resid", 512, 768, 768, 8), ("qkv", 512 * 197, 2304, 768, 8),
+    # ragged last tile rows (the half-batch streams of B = 256: M = 128 x 197)
+    ("qkv", 128 * 197, 2304, 768, 8), ("qkv", 128 * 197, 2304, 768, 4), ("gelu", 128 * 197, 3072, 768, 8),
+    ("gelu", 300, 3072, 768, 4),
+])
+def test_persistent_projection_gemm_equals_big_tile(epi_name, M, N, K, bw, monkeypatch):
+    """The persistent projection GEMM (k_proj: 256 x 256 tiles, the next tile's first
+    stages in flight during the epilogue, stores straight from the MFMA layout, residual /
+    column constants by LDS-DMA) against the one-tile-per-workgroup kernel (k_qgemm_big) on the same packed weights:
+    bit-identical for every epilogue, int8 and nibble-packed int4 weights, with many
+    tiles per workgroup (M up to 100 864 rows) and with one, ragged last tile rows; small output scales put many
+    values next to rounding boundaries (the filters' exact fallbacks run)."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_GELU, EPI_QKV, EPI_RESID, _gemm, _pack_b
+    epi = {"qkv": EPI_QKV, "resid": EPI_RESID, "gelu": EPI_GELU}[epi_name]
+    rng = np.random.default_rng(M + N + K + bw)
+    lim = 128 if bw == 8 else 8
+    a = DeviceArray.from_host(rng.integers(-lim, lim, size=(M, K), dtype=np.int8))
+    bt_h = rng.integers(-24 if bw == 8 else -8, 25 if bw == 8 else 8, size=(N, K), dtype=np.int8)
+    bt = DeviceArray.from_host(bt_h)
+    col_h = bt_h.astype(np.int64).sum(axis=1)
+    col = DeviceArray.from_host(col_h)
+    bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
+    resid = DeviceArray.from_host(rng.standard_normal((M, N)).astype(np.float32))
+    packed, kind = _pack_b(bt, bw)
+    colterm = DeviceArray.from_host((col_h * -5).astype(np.int32))
+    variants = [{"NQK_NO_PROJ": "1"}, {}]
+    if epi == EPI_RESID:  # opt-in for the residual epilogues
+        variants = [{"NQK_NO_PROJ": "1"}, {"NQK_PROJ_RESID": "1"}, {"NQK_PROJ_RESID": "1", "NQK_NO_F32X": "1"}]
+    outs, kernels = [], []
+    sa = 1.3e-4 if bw == 8 else 4e-3
+    for var in variants:
+        for k in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_PROJ_RESID"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in var.items():
+            monkeypatch.setenv(k, v)
+        e = _lib.Epilogue()
+        e.zp_flags, e.bit_width = _lib.ZP_COL, bw
+        e.zpa, e.col, e.col_absmax = -5, col.ptr, int(np.abs(col_h).max())
+        e.bias, e.b_packed, e.colterm = bias.ptr, kind, colterm.ptr
+        if epi == EPI_QKV:
+            T, H, Dh = 197, N // 3 // 64, 64
+            e.group_cols, e.tokens, e.heads, e.hdim = N // 3, T, H, Dh
+            bufs = [DeviceArray((M // T * H * T, Dh), np.int8) for _ in range(3)]
+            for g in range(3):
+                e.s_acc[g] = float(np.float32(sa * (g + 1)))
+                e.s_out[g], e.zp_out[g], e.out[g] = (0.0021, 0.0173, 0.05)[g], (3, -140, 0)[g], bufs[g].ptr
+        elif epi == EPI_RESID:
+            e.group_cols = 1 << 30
+            bufs = [DeviceArray((M, N), np.float32)]
+            e.s_acc[0], e.out[0], e.resid = float(np.float32(sa * 2)), bufs[0].ptr, resid.ptr
+        else:
+            e.group_cols = 1 << 30
+            bufs = [DeviceArray((M, N), np.int8)]
+            e.s_acc[0], e.s_out[0], e.zp_out[0], e.out[0] = float(np.float32(sa)), 0.0027, -9, bufs[0].ptr
+            e.div, e.add1, e.mul2 = float(np.float32(1.4142135381698608)), 1.0, 0.5
+        _gemm(epi, a, packed, 1, M, N, K, K, K, None, 0, 0, e)
+        kernels.append(_last_kernel())
+        outs.append([b.to_host() for b in bufs])
+    assert kernels[0] == 1 and all(k == 3 for k in kernels[1:]), kernels
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            np.testing.assert_array_equal(x, y)
