@@ -122,7 +122,7 @@ def build_vit(batch: int, bit_width: int, group, calib_batch: int = 8):
     return model, qmodel
 
 
-PROJ_TAGS = ("qgemm_qkv", "qgemm_resid", "qgemm_gelu")  # MatMuls with constant weights (k_qgemm_big)
+PROJ_TAGS = ("qgemm_qkv", "qgemm_resid", "qgemm_gelu")  # MatMuls with constant weights (k_proj / k_qgemm_big)
 
 
 def kernel_breakdown(qmodel, x_dev):
@@ -170,17 +170,20 @@ def kernel_breakdown(qmodel, x_dev):
     return out, {"ms": pm, "ops": po, "launches": pl}
 
 
-def traffic_from_profiles(kernel_prefix: str):
-    """HBM bytes per launch of the projection GEMMs from the committed PMC summary
-    (profiles/pmc_traffic.json, collected with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-    in separate passes, FETCH_SIZE doubled for gfx950 per MI355X_MICROARCH.md), or None."""
+def traffic_from_profiles(kernel_families):
+    """HBM bytes per launch of the projection GEMMs (mean over the launches of the given
+    kernel families) from the committed PMC summary (profiles/pmc_traffic.json, collected
+    with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH_SIZE doubled for
+    gfx950 per MI355X_MICROARCH.md), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         data = json.load(open(path))
     except (OSError, ValueError):
         return None
-    ent = data.get("kernels", {}).get(kernel_prefix)
-    return None if ent is None else ent.get("hbm_bytes_per_launch")
+    ents = [data.get("kernels", {}).get(k) for k in kernel_families]
+    ents = [e for e in ents if e]
+    n = sum(e["launches"] for e in ents)
+    return round(sum(e["launches"] * e["hbm_bytes_per_launch"] for e in ents) / n) if n else None
 
 
 def host_cpu() -> dict:
@@ -312,9 +315,10 @@ def run_vit(args, group):
     res["matmul_tops"] = round(achieved, 2)
     res["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(INT8_PEAK_TOPS, 1),
                        "unit": "TOPS", "frac": round(achieved / INT8_PEAK_TOPS, 4),
-                       "traffic": traffic_from_profiles("k_qgemm_big") if bw == 8 else None,
-                       "kernel": "k_qgemm_big: the 48 int8 MFMA projection GEMMs of one forward (QKV, attention "
-                                 "output, FFN up + GELU, FFN down; fused epilogues), 2*M*N*K int8 ops per launch",
+                       "traffic": traffic_from_profiles(("k_proj", "k_qgemm_big")) if bw == 8 else None,
+                       "kernel": "the 48 int8 MFMA projection GEMMs of one forward, fused epilogues: k_proj "
+                                 "(persistent 256x256 tiles: QKV, FFN up + GELU) and k_qgemm_big (attention output, "
+                                 "FFN down + residual); 2*M*N*K int8 ops per launch",
                        "launches": proj["launches"], "avg_launch_us": round(1e3 * proj["ms"] / max(1, proj["launches"]), 2),
                        "gemm_ms_per_forward": round(proj["ms"], 3)}
     res["kernels"] = kern

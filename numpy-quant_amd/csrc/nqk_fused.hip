@@ -1778,17 +1778,17 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     const bool f32x = i32 && (epi == EPI_QKV || (epi == EPI_GELU && e.gelu_filter)) && zp_small &&
                       16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
     const bool use_pp = pp && !params->b_packed;
-    // the persistent 256 x 256 kernel where it takes the shape (QKV / GELU; the residual
-    // epilogues only with NQK_PROJ_RESID=1: their f32 residual read + output write is HBM
-    // traffic the one-tile-per-workgroup kernel overlaps better);
-    // NQK_NO_PROJ=1 keeps the one-tile-per-workgroup kernel
+    // the persistent 256 x 256 kernel where it takes the shape: QKV by default; FFN-up +
+    // GELU with NQK_PROJ_GELU=1 and the residual epilogues with NQK_PROJ_RESID=1 (faster
+    // alone, not inside the two-stream forward, DESIGN.md "Projection GEMM variants");
+    // NQK_NO_PROJ=1 keeps the one-tile-per-workgroup kernel everywhere
     const bool f32x_r = i32 && epi == EPI_RESID && 16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
     const bool proj_shape = params->b_packed && i32 && params->colterm != nullptr && M >= 256 && (M % 256 == 0 || epi != EPI_RESID) && N % GBN == 0 &&
                             (K == 768 || K == 3072) && (double)M * N * 4.0 < 4294967295.0 && (double)M * lda < 4294967295.0 &&
                             !getenv("NQK_NO_PROJ") &&
                             ((epi == EPI_RESID && !(params->b_packed == 2 && K == 768) && getenv("NQK_PROJ_RESID")) ||
                              (f32x && K == 768 &&
-                              (epi == EPI_GELU ||
+                              ((epi == EPI_GELU && getenv("NQK_PROJ_GELU")) ||
                                (epi == EPI_QKV && params->tokens >= 64 && params->hdim == 64 && params->group_cols % 128 == 0 &&
                                 (double)M * params->heads * params->hdim < 2147483647.0))));
     if (proj_shape) {

@@ -247,10 +247,12 @@ def test_persistent_projection_gemm_equals_big_tile(epi_name, M, N, K, bw, monke
     variants = [{"NQK_NO_PROJ": "1"}, {}]
     if epi == EPI_RESID:  # opt-in for the residual epilogues
         variants = [{"NQK_NO_PROJ": "1"}, {"NQK_PROJ_RESID": "1"}, {"NQK_PROJ_RESID": "1", "NQK_NO_F32X": "1"}]
+    elif epi == EPI_GELU:  # opt-in
+        variants = [{"NQK_NO_PROJ": "1"}, {"NQK_PROJ_GELU": "1"}]
     outs, kernels = [], []
     sa = 1.3e-4 if bw == 8 else 4e-3
     for var in variants:
-        for k in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_PROJ_RESID"):
+        for k in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_PROJ_RESID", "NQK_PROJ_GELU"):
             monkeypatch.delenv(k, raising=False)
         for k, v in var.items():
             monkeypatch.setenv(k, v)

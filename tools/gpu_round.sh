@@ -21,6 +21,16 @@ if [ "${PROFILE:-0}" = "1" ]; then
   timeout -k 10 ${PROF_TIMEOUT:-400} rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
   rc=$?
   echo "rocprof rc=$rc" >> gpurun_out/prof_bench.err
-  exit $rc
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+if [ "${PMC:-0}" = "1" ]; then
+  # HBM traffic per kernel: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots)
+  for c in FETCH_SIZE WRITE_SIZE; do
+    rm -rf gpurun_out/pmc_bench_$c
+    timeout -s KILL 180 rocprofv3 --pmc $c --kernel-trace -d gpurun_out/pmc_bench_$c -o run --output-format csv -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_bench_$c.log 2>&1
+    rc=$?
+    echo "pmc $c rc=$rc" >> gpurun_out/pmc_bench_$c.log
+    if [ $rc -ne 0 ]; then exit $rc; fi
+  done
 fi
 exit 0
