@@ -1525,6 +1525,108 @@ k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const f
   }
 }
 
+// The same register tree, with the rows moved through LDS so that every global load and
+// store of a wave is one contiguous 1 KiB (the tree's lane layout reads 16 B at a 32-B
+// stride: 8 segments per row and instruction).  A wave's RW = 64 / (2 NL) rows are
+// contiguous in memory: loaded linearly into the wave's own LDS image (16 B of pad per
+// 96-column leaf: conflict-free reads in the tree layout), read in the tree layout,
+// and the packed int8 results written back into LDS (784-B rows: conflict-free dword
+// writes) and stored linearly.  No workgroup barrier: each wave owns its LDS image.
+template <int NL>
+__global__ void __launch_bounds__(256)
+k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
+               int8_t* __restrict__ out, int64_t rows, float eps, float s, double rs, double zp, double lo,
+               double hi) {
+  constexpr int LF = 96, LPR = NL * 2, NI = LF / 8, COLS = NL * LF, RW = 64 / LPR;
+  constexpr int CH = COLS / 4;                      // 16-B chunks per row
+  constexpr int RSI = COLS * 4 + NL * 16;           // LDS bytes per input row
+  constexpr int RSO = COLS + 16;                    // LDS bytes per output row
+  constexpr int WLDS = RW * RSI;                    // >= RW * RSO
+  constexpr int NLD = RW * CH / 64, NST = RW * COLS / 16 / 64;
+  static_assert(RW * CH % 64 == 0 && RW * COLS % 1024 == 0, "k_ln_quant_lds: shape");
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int8_t* const wl = lds + wave * WLDS;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * RW;
+  if (row0 >= rows) return;  // (uniform per wave; no workgroup barrier follows)
+  // ---- linear loads (rows past the end read the last row; not stored)
+  float4 ld[NLD];
+#pragma unroll
+  for (int k = 0; k < NLD; ++k) {
+    const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
+    const int64_t gr = row0 + r < rows ? row0 + r : rows - 1;
+    ld[k] = *reinterpret_cast<const float4*>(x + gr * COLS + c * 4);
+  }
+#pragma unroll
+  for (int k = 0; k < NLD; ++k) {
+    const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
+    *reinterpret_cast<float4*>(wl + r * RSI + c * 16 + (c / (LF / 4)) * 16) = ld[k];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  // ---- the tree layout: lane (row r, leaf, grp) holds columns leaf*96 + 8i + 4grp + 0..3
+  const int r = lane / LPR, u = lane % LPR, leaf = u >> 1, grp = u & 1;
+  const int c0 = leaf * LF + 4 * grp;
+  float4 xv[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    xv[i] = *reinterpret_cast<const float4*>(wl + r * RSI + (leaf * (LF / 4) + 2 * i + grp) * 16 + leaf * 16);
+  float a0 = xv[0].x, a1 = xv[0].y, a2 = xv[0].z, a3 = xv[0].w;
+#pragma unroll
+  for (int i = 1; i < NI; ++i) {
+    a0 = a0 + xv[i].x; a1 = a1 + xv[i].y; a2 = a2 + xv[i].z; a3 = a3 + xv[i].w;
+  }
+  float acc = (a0 + a1) + (a2 + a3);
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) acc = acc + __shfl_xor(acc, m, 64);
+  const float fcols = (float)COLS;
+  const float nmean = -(acc / fcols);
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    xv[i].x = xv[i].x + nmean; xv[i].y = xv[i].y + nmean; xv[i].z = xv[i].z + nmean; xv[i].w = xv[i].w + nmean;
+  }
+  a0 = xv[0].x * xv[0].x; a1 = xv[0].y * xv[0].y; a2 = xv[0].z * xv[0].z; a3 = xv[0].w * xv[0].w;
+#pragma unroll
+  for (int i = 1; i < NI; ++i) {
+    a0 = a0 + xv[i].x * xv[i].x; a1 = a1 + xv[i].y * xv[i].y;
+    a2 = a2 + xv[i].z * xv[i].z; a3 = a3 + xv[i].w * xv[i].w;
+  }
+  float v2 = (a0 + a1) + (a2 + a3);
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) v2 = v2 + __shfl_xor(v2, m, 64);
+  const float var = v2 / fcols;
+  const float inv = 1.0f / __builtin_sqrtf(var + eps);
+  // every lane's tree reads are done before the image is overwritten (in-order LDS)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const float4 gg = *reinterpret_cast<const float4*>(g + c0 + 8 * i);
+    const float4 bb = *reinterpret_cast<const float4*>(b + c0 + 8 * i);
+    const float y[4] = {((xv[i].x * inv) * gg.x) + bb.x, ((xv[i].y * inv) * gg.y) + bb.y,
+                        ((xv[i].z * inv) * gg.z) + bb.z, ((xv[i].w * inv) * gg.w) + bb.w};
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float t = (float)((double)y[k] * rs);
+      const double uu = zp + (double)t;
+      const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
+      packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(wl + r * RSO + c0 + 8 * i) = packed;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  // ---- linear stores
+#pragma unroll
+  for (int k = 0; k < NST; ++k) {
+    const int C = k * 64 + lane, rr = C / (COLS / 16), c = C - rr * (COLS / 16);
+    const v4i v = *reinterpret_cast<const v4i*>(wl + rr * RSO + c * 16);
+    if (row0 + rr < rows) *reinterpret_cast<v4i*>(out + (row0 + rr) * COLS + c * 16) = v;
+  }
+}
+constexpr int ln_lds_bytes(int nl) { return 4 * (64 / (2 * nl)) * (nl * 96 * 4 + nl * 16); }
+
 // ------------------------------------------------------------------ Softmax + quantize
 // one row per wave; output row stride ldo (>= cols, pad zero-filled); optional row sums
 __global__ void __launch_bounds__(256)
@@ -1856,6 +1958,12 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
     const double rs = 1.0 / (double)scale;
     const int64_t lanes = rows * p.nleaf * 2;
     const unsigned grid = (unsigned)((lanes + 255) / 256);
+    if (p.nleaf == 8 && !getenv("NQK_LN_REG")) {  // rows through LDS: linear 1 KiB loads / stores per wave
+      const unsigned g8 = (unsigned)((rows + 15) / 16);
+      hipLaunchKernelGGL((k_ln_quant_lds<8>), dim3(g8), dim3(256), ln_lds_bytes(8), stream(), x, gamma, beta, out,
+                         rows, eps, scale, rs, (double)zp, lo, hi);
+      return launch_status("nqk_ln_quant(lds)");
+    }
     switch (p.nleaf) {
       case 8: hipLaunchKernelGGL((k_ln_quant_reg<8>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
                                  eps, scale, rs, (double)zp, lo, hi); break;
