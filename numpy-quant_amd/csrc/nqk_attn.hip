@@ -22,6 +22,9 @@
 #ifndef NQK_ATTN_DIAG
 #define NQK_ATTN_DIAG 0
 #endif
+#ifndef NQK_ATTN_EXPW
+#define NQK_ATTN_EXPW 4
+#endif
 
 namespace nqk {
 namespace {
@@ -99,6 +102,9 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             int8_t* __restrict__ ctx, AttnArgs a) {
   constexpr int TP = NT * 32;  // padded tokens (score columns / PV contraction)
   constexpr int G = TP / 8;    // 8-column groups of a score row
+  // group qq of score tile c (columns c*32 + 8qq .. + 7 of both halves) past the last
+  // token: known at compile time when the token count is
+  auto pad_group = [](int c, int qq) constexpr { return TC > 0 && c * 32 + 8 * qq >= TC; };
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int T = TC ? TC : a.T, PST = TC ? NT * 32 + 16 : a.PST;
   int8_t* Ks = lds;
@@ -119,7 +125,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     const v4i kv = row < T ? *reinterpret_cast<const v4i*>(k + row * 64 + ch * 16) : z;
     const v4i vv = row < T ? *reinterpret_cast<const v4i*>(v + row * 64 + ch * 16) : z;
     *reinterpret_cast<v4i*>(Ks + swz64a(row, ch)) = kv;
-#if NQK_ATTN_DIAG  // diagnostic builds only: V^T staging skipped (wrong context)
+#if NQK_ATTN_DIAG & 1  // diagnostic builds only (wrong results): 1 = V^T staging skipped, 2 = exp
+                      // replaced by one add, 4 = P quantize replaced by a convert
     if (row == 0) Vt[ch] = (int8_t)vv[0];
 #else
 #pragma unroll
@@ -164,30 +171,32 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     int rq = sum16a(qb[0]) + sum16a(qb[1]);
     rq += xor32i(rq);
     const int rowterm = rq * a.zk;
-    // ---- S^T = K Q^T
-    v16i acc[NT];
-#pragma unroll
-    for (int c = 0; c < NT; ++c) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[c][r] = 0;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const v4i ka = *reinterpret_cast<const v4i*>(Ks + swz64a(c * 32 + r32, 2 * s + h));
-        acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ka, qb[s], acc[c], 0, 0, 0);
-      }
-    }
-    // ---- dequant + Div (EPI_SCORES), row max
+    // ---- per score tile c: S^T = K Q^T (two MFMAs), dequant + Div (EPI_SCORES), row
+    // max; only one tile's accumulators are live
     float e[NT][16];
     float mx = -__builtin_inff();
 #pragma unroll
-    for (int c = 0; c < NT; ++c)
+    for (int c = 0; c < NT; ++c) {
+      v16i acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const v4i ka = *reinterpret_cast<const v4i*>(Ks + swz64a(c * 32 + r32, 2 * s + h));
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(ka, qb[s], acc, 0, 0, 0);
+      }
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
+        if (pad_group(c, qq)) {  // every column of the group is padding (compile time)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) e[c][4 * qq + j] = 0.0f;
+          continue;
+        }
         const v4i ck = *reinterpret_cast<const v4i*>(colK + c * 32 + 8 * qq + 4 * h);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * qq + j, n = c * 32 + 8 * qq + 4 * h + j;
-          const int vv = acc[c][r] - rowterm - ck[j];
+          const int vv = acc[r] - rowterm - ck[j];
           float y;
           // FAST: RN(v s) / 2^k == RN(v (s / 2^k)) while both are normal (host-checked)
           if constexpr (FAST) y = (float)vv * a.s_qkd;
@@ -199,6 +208,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+    }
     {
       const float o = xor32f(mx);
       mx = o > mx ? o : mx;
@@ -208,8 +218,11 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     for (int c = 0; c < NT; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        e[c][r] = np_expf_nonpos(e[c][r] + nm);  // y - max <= 0; -inf pads -> 0
-        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        if (pad_group(c, r >> 2)) continue;  // stays 0
+        if constexpr ((NQK_ATTN_DIAG & 2) != 0) e[c][r] = e[c][r] + nm;
+        else e[c][r] = np_expf_nonpos(e[c][r] + nm);  // y - max <= 0; -inf pads -> 0
+        // scheduling window of NQK_ATTN_EXPW independent exp chains
+        if ((r % NQK_ATTN_EXPW) == NQK_ATTN_EXPW - 1) __builtin_amdgcn_sched_barrier(0);
       }
     // ---- NumPy pairwise sum: accumulators r[4h + j] of each leaf, in increasing n
     float ra[2][4], tv[2][4];
@@ -255,24 +268,76 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     const float tot = n2 ? leaf[0] + leaf[1] : leaf[0];
     const double rtot = 1.0 / (double)tot;
     const float kpf = (float)(rtot * a.rs_p);  // t = e / tot / s_p within |t| 2^-22 of e * kpf
-    // ---- P = quantize(e / tot): 4 packed bytes per (tile, group), row sums
-    int dw[NT][4];
+    // the filter's bound for the whole row (|tf| <= kpf (1 + 2^-23)), with margin
+    const float plim = 0.5f - 2.0f * __builtin_fmaf(kpf, 0x1p-21f, 0x1p-126f);
+    const float zp128 = a.zp_p_f + 128.0f, lo128 = a.lo_f + 128.0f, hi128 = a.hi_f + 128.0f;
+    // ---- per score tile c: P = quantize(e / tot) (4 packed bytes per group, row sums),
+    // then at once its share of O^T = V^T P^T (B operand = P row m, 16 consecutive tokens
+    // per half), so only one tile's packed P is live
     int rp = 0;
+    v16i acc2[2];
 #pragma unroll
-    for (int c = 0; c < NT; ++c)
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2[j][r] = 0;
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      int dw[4];
+      if constexpr (FAST && (NQK_ATTN_DIAG & 4) == 0) {
+        // t = e / tot / s_p is within thr of tf = e * kpf (|tf| <= kpf: e <= 1); where tf
+        // is farther than that from a rounding boundary, rint(tf) is rint(t).  Per
+        // element: the product, rint, the distance test, then v + 128 (v = the clamped
+        // integer, in [0, 255]) converted straight into its byte (v_cvt_pk_u8_f32) and
+        // the bytes flipped to two's complement at once (^ 0x80 each).
+        uint32_t slow = 0;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          if (pad_group(c, qq)) {
+            dw[qq] = 0;
+            continue;
+          }
+          uint32_t packed = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = c * 32 + 8 * qq + 4 * h + j;
+            const float tf = e[c][4 * qq + j] * kpf;
+            const float r = __builtin_rintf(tf);
+            slow |= (uint32_t)!(__builtin_fabsf(tf - r) < plim) << (4 * qq + j);
+            float v = __builtin_amdgcn_fmed3f(r + zp128, lo128, hi128);
+            v = n < T ? v : 128.0f;  // padded columns: 0
+            packed = __builtin_amdgcn_cvt_pk_u8_f32(v, j, packed);
+          }
+          dw[qq] = (int)(packed ^ 0x80808080u);
+        }
+        if (__builtin_expect(__any(slow != 0), 0)) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            if (pad_group(c, qq)) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int n = c * 32 + 8 * qq + 4 * h + j;
+              if ((slow >> (4 * qq + j)) & 1) {
+                const int qv = n < T ? quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) : 0;
+                dw[qq] = (int)(((uint32_t)dw[qq] & ~(0xffu << (8 * j))) | ((uint32_t)(qv & 0xff) << (8 * j)));
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          if (!pad_group(c, qq)) rp = __builtin_amdgcn_sdot4(dw[qq], 0x01010101, rp, false);
+      } else {
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
+        if (pad_group(c, qq)) {
+          dw[qq] = 0;
+          continue;
+        }
         uint32_t packed = 0;
         int qs[4];
-        if constexpr (FAST) {
-          bool sl[4];
+        if constexpr ((NQK_ATTN_DIAG & 4) != 0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) qs[j] = quant_filter(e[c][4 * qq + j] * kpf, a.zp_p_f, a.lo_f, a.hi_f, &sl[j]);
-          if (__builtin_expect(__any(sl[0] | sl[1] | sl[2] | sl[3]), 0)) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (sl[j]) qs[j] = quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi);
-          }
+          for (int j = 0; j < 4; ++j) qs[j] = (int)e[c][4 * qq + j];
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -285,31 +350,24 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           rp += qv;
           packed |= ((uint32_t)(qv & 0xff)) << (8 * j);
         }
-        dw[c][qq] = (int)packed;
+        dw[qq] = (int)packed;
         __builtin_amdgcn_sched_barrier(0);
       }
-    rp += xor32i(rp);
-    // ---- O^T = V^T P^T: B operand = P row m, 16 consecutive tokens per half
-    v16i acc2[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc2[j][r] = 0;
-#pragma unroll
-    for (int c = 0; c < NT; ++c) {
+      }
       // half 0 needs tokens 0..15 of the tile = [own g0, partner g0, own g1, partner g1];
       // half 1 needs 16..31 = [partner g2, own g2, partner g3, own g3]
-      const int xa = xor32i(h ? dw[c][0] : dw[c][2]);
-      const int xb = xor32i(h ? dw[c][1] : dw[c][3]);
+      const int xa = xor32i(h ? dw[0] : dw[2]);
+      const int xb = xor32i(h ? dw[1] : dw[3]);
       v4i pb;
-      if (h) { pb[0] = xa; pb[1] = dw[c][2]; pb[2] = xb; pb[3] = dw[c][3]; }
-      else   { pb[0] = dw[c][0]; pb[1] = xa; pb[2] = dw[c][1]; pb[3] = xb; }
+      if (h) { pb[0] = xa; pb[1] = dw[2]; pb[2] = xb; pb[3] = dw[3]; }
+      else   { pb[0] = dw[0]; pb[1] = xa; pb[2] = dw[1]; pb[3] = xb; }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const v4i va = *reinterpret_cast<const v4i*>(Vt + (j * 32 + r32) * PST + (2 * c + h) * 16);
         acc2[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(va, pb, acc2[j], 0, 0, 0);
       }
     }
+    rp += xor32i(rp);
     // ---- dequant + quantize (EPI_PV) -> ctx[img][m][head * 64 + d], 4 dims per store
     const int rowp = rp * a.zv;
     int8_t* orow = ctx + ((int64_t)img * T + m) * a.ld_out + head * 64;

@@ -1,0 +1,95 @@
+"""The calibration cone, bounded.
+
+Model.quantize (reference model.py:328-442) calibrates on a float forward whose MatMuls
+are OpenBLAS np.matmul (reference tensor.py:100-101).  The device float forward equals
+it bit for bit for every MatMul with K <= 768; OpenBLAS's summation order for the K = 3072
+FFN-down MatMul is not reproduced, so the values downstream of it (the "cone",
+tests/test_gpu_models.py:tainted_values) differ by ulps, and so may the quantization
+parameters calibrated on them.  This test measures and bounds that gap on the
+reference's own fixtures (tests/golden/vit_b1 and layer_b1, recorded from the
+reference):
+
+  * every scale outside the cone is bit-identical, and inside it at most SCALE_ULPS
+    float32 ulps from the reference's;
+  * every zero point inside the cone within 1 of the reference's;
+  * the output of the device-calibrated QModel on the reference's run input against the
+    reference's output (both dequantized float32): no element more than OUT_MAX_STEPS
+    quantization steps of the output away, at most OUT_STEP_BUDGET of them more than half
+    a step.  (north_star's 1e-5 does not hold inside the cone: every element's
+    dequantizing scale differs by ulps, and integers flip at rounding boundaries.)
+
+The bounds were set from the measured gap with margin (values in the assertion
+messages); the gap is recorded in DESIGN.md §3."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from test_gpu_models import tainted_values
+
+pytestmark = pytest.mark.gpu
+MODELS = os.path.join(ROOT, "numpy-quant_amd", "models")
+# measured (MI355X, this fixture): layer_b1 3 of 4 cone scales differ by <= 2 ulps, zero
+# points equal, output bit-identical; vit_b1 318 of 438 cone scales differ by <= 8 ulps,
+# zero points equal, 58.5 % of the 1000 logits off by 1-3 output steps (0.015 each)
+SCALE_ULPS = 32
+OUT_MAX_STEPS = 4         # largest |device - reference| output difference, in output quantization steps
+OUT_STEP_BUDGET = 0.75    # fraction of output elements allowed to be off by more than half a step
+
+
+def _bits(scale):
+    return int(np.asarray(scale, np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("tag,fname", [
+    ("layer_b1", "vit_image_classifier_encoder_layer_no_weights.onnx"),
+    ("vit_b1", "vit_image_classifier_no_weights.onnx"),
+])
+def test_calibration_cone_is_bounded(tag, fname):
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model
+    meta = json.load(open(os.path.join(GOLDEN, f"{tag}.json")))
+    arrs = np.load(os.path.join(GOLDEN, f"{tag}.npz"))
+    proto = onnx_proto.load(os.path.join(MODELS, fname), synthetic_weights=True, seed=meta["seed"])
+    model = Model.from_onnx(proto)
+    bw_key = [k for k in meta if k.startswith("bw")][0]
+    bw = int(bw_key[2:])
+    qmodel = model.quantize([arrs["x_cal"]], bit_width=bw)
+    taint = tainted_values(model)
+    ref = meta[bw_key]["qparams"]
+    ulps, dzp, outside = [], [], []
+    for name, r in ref.items():
+        p = qmodel.quant_params[name]
+        du = abs(_bits(p.scale) - r["scale_bits"])
+        z = None if p.zero_point is None else int(p.zero_point)
+        dz = 0 if (z is None and r["zp"] is None) else abs((z or 0) - (r["zp"] or 0))
+        if name not in taint:
+            if du or dz:
+                outside.append(name)
+            continue
+        ulps.append(du)
+        dzp.append(dz)
+    assert not outside, f"parameters differing outside the cone: {outside[:8]}"
+    n_scale = sum(u > 0 for u in ulps)
+    n_zp = sum(d > 0 for d in dzp)
+    msg = (f"{tag}: cone of {len(ulps)} parameters: {n_scale} scales differ (max {max(ulps, default=0)} ulps), "
+           f"{n_zp} zero points differ (max {max(dzp, default=0)})")
+    print(msg)
+    assert max(ulps, default=0) <= SCALE_ULPS, msg
+    assert max(dzp, default=0) <= 1, msg
+    out = np.asarray(qmodel([arrs["x_run"]])[0], dtype=np.float32)
+    want = np.asarray(arrs[f"{bw_key}_out"], dtype=np.float32)
+    assert out.shape == want.shape
+    diff = np.abs(out - want)
+    # in quantization steps of the output (the reference's scale of the graph output)
+    oname = model.outputs[0].name
+    step = float(np.uint32(ref[oname]["scale_bits"]).view(np.float32)) if oname in ref else float(np.abs(want).max()) / 127
+    steps = diff / step
+    frac_1e5 = float(np.mean(diff > 1e-5))
+    frac_step = float(np.mean(steps > 0.5))
+    msg2 = (f"{tag}: output |diff| max {diff.max():.3g} = {steps.max():.2f} output steps ({step:.3g}); "
+            f"{frac_1e5:.2%} of {diff.size} elements beyond 1e-5, {frac_step:.2%} beyond half a step")
+    print(msg2)
+    assert steps.max() <= OUT_MAX_STEPS and frac_step <= OUT_STEP_BUDGET, msg2
