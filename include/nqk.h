@@ -138,7 +138,7 @@ int nqk_qgemm_generic(const void* a, int a_dtype, const void* b, int b_dtype, in
 
 /* ------------------------------------------- float32 GEMM (BLAS-order exact) */
 /* C = A[M][K] . B[K][N] (element strides a_sm/a_sk, b_sk/b_sn).  Every output element is the
- * reference BLAS's summation: K is cut into OpenBLAS level-3 blocks (GEMM_Q=384
+ * reference BLAS's summation: K is cut into OpenBLAS level-3 blocks (GEMM_Q=448
  * rule), each block a k-ordered fmaf chain from 0, blocks added in order.  Used
  * by Conv (numpy_helper.py:73-92 x.dot(w)) and by float MatMul/Gemm of the
  * calibration forward (model.py:153-157, 122-131 via np.matmul). */

@@ -8,9 +8,10 @@
 //  * nqk_sgemm        — float32 GEMM that reproduces the reference BLAS bit for
 //                       bit: OpenBLAS (scipy-openblas 0.3.29, SkylakeX kernels, the
 //                       one NumPy 2.2.6 ships on both hosts) cuts K into level-3
-//                       blocks (GEMM_Q = 384; a remainder in (Q, 2Q) is halved),
+//                       blocks (GEMM_Q = 448; a remainder in (Q, 2Q) is halved),
 //                       each block a k-ordered fmaf chain from 0, blocks summed in
-//                       order.  Verified against np.dot for K <= 768.
+//                       order.  Verified against np.matmul for K = 64 .. 3072
+//                       (tests/test_host.py::test_blas_order_matches_numpy_matmul).
 //  * nqk_im2col       — numpy_helper.py:18-70 sliding windows, NCHW input.
 #include "nqk_common.h"
 
@@ -438,9 +439,10 @@ __global__ void k_im2col(const float* __restrict__ x, float* __restrict__ cols, 
 
 }  // namespace
 
-// OpenBLAS level-3 K blocking (driver/level3/level3.c): GEMM_Q = 384 for SkylakeX sgemm
+// OpenBLAS level-3 K blocking (driver/level3/level3.c): GEMM_Q = 448 for SkylakeX sgemm
+// (identified against np.matmul: 384 agrees only while K <= 768)
 static int blas_kblocks(int64_t K, KBlocks* kb) {
-  const int64_t Q = 384, U = 2;
+  const int64_t Q = 448, U = 2;
   int64_t ls = 0;
   kb->n = 0;
   while (ls < K) {

@@ -1,25 +1,25 @@
 """The calibration cone, bounded.
 
 Model.quantize (reference model.py:328-442) calibrates on a float forward whose MatMuls
-are OpenBLAS np.matmul (reference tensor.py:100-101).  The device float forward equals
-it bit for bit for every MatMul with K <= 768; OpenBLAS's summation order for the K = 3072
-FFN-down MatMul is not reproduced, so the values downstream of it (the "cone",
-tests/test_gpu_models.py:tainted_values) differ by ulps, and so may the quantization
-parameters calibrated on them.  This test measures and bounds that gap on the
-reference's own fixtures (tests/golden/vit_b1 and layer_b1, recorded from the
-reference):
+are OpenBLAS np.matmul (reference tensor.py:100-101).  The device float forward
+(nqk_sgemm: OpenBLAS's GEMM_Q = 448 K blocks, k-ordered fma chains) equals it bit for
+bit for every GEMM with more than one row, any K.  A one-row product (the classifier
+Gemm on the CLS token) runs in OpenBLAS as sgemv, whose order is not reproduced, so
+the values downstream of it (the "cone", tests/test_gpu_models.py:tainted_values) may
+differ by ulps, and so may the quantization parameters calibrated on them.  This test
+bounds that gap on the reference's own fixtures (tests/golden/vit_b1 and layer_b1,
+recorded from the reference):
 
   * every scale outside the cone is bit-identical, and inside it at most SCALE_ULPS
     float32 ulps from the reference's;
   * every zero point inside the cone within 1 of the reference's;
   * the output of the device-calibrated QModel on the reference's run input against the
-    reference's output (both dequantized float32): no element more than OUT_MAX_STEPS
-    quantization steps of the output away, at most OUT_STEP_BUDGET of them more than half
-    a step.  (north_star's 1e-5 does not hold inside the cone: every element's
-    dequantizing scale differs by ulps, and integers flip at rounding boundaries.)
+    reference's output (both dequantized float32) within north_star's 1e-5.
 
-The bounds were set from the measured gap with margin (values in the assertion
-messages); the gap is recorded in DESIGN.md §3."""
+Measured on MI355X: layer_b1 has an empty cone (bit-identical); vit_b1 one parameter
+(the logits' scale, 4 ulps), logits within 4.8e-7.  (With GEMM_Q = 384, as in round 1,
+the K = 3072 FFN-down MatMuls joined the cone: 318 of 438 scales off by up to 8 ulps
+and 58.5 % of the logits off by 1-3 output steps.)"""
 import json
 import os
 
@@ -31,12 +31,8 @@ from test_gpu_models import tainted_values
 
 pytestmark = pytest.mark.gpu
 MODELS = os.path.join(ROOT, "numpy-quant_amd", "models")
-# measured (MI355X, this fixture): layer_b1 3 of 4 cone scales differ by <= 2 ulps, zero
-# points equal, output bit-identical; vit_b1 318 of 438 cone scales differ by <= 8 ulps,
-# zero points equal, 58.5 % of the 1000 logits off by 1-3 output steps (0.015 each)
-SCALE_ULPS = 32
-OUT_MAX_STEPS = 4         # largest |device - reference| output difference, in output quantization steps
-OUT_STEP_BUDGET = 0.75    # fraction of output elements allowed to be off by more than half a step
+SCALE_ULPS = 16
+OUT_ATOL = 1e-5           # north_star's tolerance on dequantized float outputs
 
 
 def _bits(scale):
@@ -83,13 +79,6 @@ def test_calibration_cone_is_bounded(tag, fname):
     want = np.asarray(arrs[f"{bw_key}_out"], dtype=np.float32)
     assert out.shape == want.shape
     diff = np.abs(out - want)
-    # in quantization steps of the output (the reference's scale of the graph output)
-    oname = model.outputs[0].name
-    step = float(np.uint32(ref[oname]["scale_bits"]).view(np.float32)) if oname in ref else float(np.abs(want).max()) / 127
-    steps = diff / step
-    frac_1e5 = float(np.mean(diff > 1e-5))
-    frac_step = float(np.mean(steps > 0.5))
-    msg2 = (f"{tag}: output |diff| max {diff.max():.3g} = {steps.max():.2f} output steps ({step:.3g}); "
-            f"{frac_1e5:.2%} of {diff.size} elements beyond 1e-5, {frac_step:.2%} beyond half a step")
+    msg2 = f"{tag}: output |diff| max {diff.max():.3g}, {float(np.mean(diff > 0)):.2%} of {diff.size} elements differ"
     print(msg2)
-    assert steps.max() <= OUT_MAX_STEPS and frac_step <= OUT_STEP_BUDGET, msg2
+    assert diff.max() <= OUT_ATOL, msg2

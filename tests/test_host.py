@@ -88,7 +88,7 @@ def test_reshape_target_and_pool_rounding():
     assert _Pool.round(3 << 20) >= 3 << 20
 
 
-def blas_blocks(K, Q=384, U=2):
+def blas_blocks(K, Q=448, U=2):
     out, ls = [], 0
     while ls < K:
         m = K - ls
@@ -102,10 +102,45 @@ def blas_blocks(K, Q=384, U=2):
 
 
 def test_blas_blocking_rule_matches_numpy_dot():
-    """The k-ordered fma chain in OpenBLAS K blocks (what nqk_sgemm computes) is
-    bit-identical to np.dot for K <= 768 (emulated here with float64 fma-free
-    steps is not possible, so use a tiny C-free check: block structure only)."""
+    """The block structure nqk_sgemm uses (OpenBLAS level-3 K loop, GEMM_Q = 448)."""
     assert blas_blocks(768) == [384, 384]
     assert blas_blocks(500) == [250, 250]
     assert blas_blocks(700) == [350, 350]
     assert blas_blocks(64) == [64]
+    assert blas_blocks(3072) == [448] * 5 + [416, 416]
+    assert blas_blocks(1536) == [448, 448, 320, 320]
+
+
+def _fma_chain_blocks(a, w, K):
+    """Per output element: a k-ordered f32 fma chain from 0 in every BLAS block, block
+    results added in order (a*b is exact in f64 for f32 operands; one f64 add then the
+    f32 rounding stands in for the fused rounding)."""
+    f32 = lambda x: x.astype(np.float32).astype(np.float64)  # noqa: E731
+    acc = np.zeros((a.shape[0], w.shape[1]))
+    ls = 0
+    for m in blas_blocks(K):
+        c = np.zeros_like(acc)
+        for k in range(ls, ls + m):
+            c = f32(a[:, k:k + 1] * w[k:k + 1, :] + c)
+        acc = f32(acc + c)
+        ls += m
+    return acc
+
+
+@pytest.mark.parametrize("K", [384, 768, 1000, 3072])
+def test_blas_order_matches_numpy_matmul(K):
+    """nqk_sgemm's summation order (GEMM_Q = 448 K blocks, k-ordered fma chains) is the
+    order of the NumPy the reference runs on (scipy-openblas 0.3.29, SkylakeX kernels):
+    an emulation of it equals np.matmul bit for bit on the FFN-down shape (K = 3072) and
+    the others.  Skipped where OpenBLAS picks other kernels."""
+    threadpoolctl = pytest.importorskip("threadpoolctl")
+    info = [i for i in threadpoolctl.threadpool_info() if i.get("internal_api") == "openblas"]
+    if not info or info[0].get("architecture") != "SkylakeX":
+        pytest.skip("OpenBLAS does not run its SkylakeX kernels on this host")
+    rng = np.random.default_rng(K)
+    A = np.maximum(rng.standard_normal((40, K)).astype(np.float32), -0.17)
+    W = (0.02 * rng.standard_normal((K, 64))).astype(np.float32)
+    C = A @ W
+    rows, cols = np.arange(0, 40, 5), np.arange(0, 64, 9)
+    got = _fma_chain_blocks(A[rows].astype(np.float64), W[:, cols].astype(np.float64), K)
+    np.testing.assert_array_equal(got.astype(np.float32), C[np.ix_(rows, cols)])
