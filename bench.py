@@ -317,7 +317,7 @@ def run_vit(args, group):
                        "unit": "TOPS", "frac": round(achieved / INT8_PEAK_TOPS, 4),
                        "traffic": traffic_from_profiles(("k_proj", "k_qgemm_big")) if bw == 8 else None,
                        "kernel": "the 48 int8 MFMA projection GEMMs of one forward, fused epilogues: k_proj "
-                                 "(persistent 256x256 tiles: QKV, FFN up + GELU) and k_qgemm_big (attention output, "
+                                 "(persistent 256x256 tiles: QKV) and k_qgemm_big (FFN up + GELU, attention output, "
                                  "FFN down + residual); 2*M*N*K int8 ops per launch",
                        "launches": proj["launches"], "avg_launch_us": round(1e3 * proj["ms"] / max(1, proj["launches"]), 2),
                        "gemm_ms_per_forward": round(proj["ms"], 3)}

@@ -24,10 +24,11 @@ if [ "${PROFILE:-0}" = "1" ]; then
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
 if [ "${PMC:-0}" = "1" ]; then
-  # HBM traffic per kernel: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots)
+  # HBM traffic per kernel: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots), one
+  # stream (whole-batch launches, as bench.py's per-kernel timings)
   for c in FETCH_SIZE WRITE_SIZE; do
     rm -rf gpurun_out/pmc_bench_$c
-    timeout -s KILL 180 rocprofv3 --pmc $c --kernel-trace -d gpurun_out/pmc_bench_$c -o run --output-format csv -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_bench_$c.log 2>&1
+    NQK_SPLIT=0 timeout -s KILL 180 rocprofv3 --pmc $c --kernel-trace -d gpurun_out/pmc_bench_$c -o run --output-format csv -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_bench_$c.log 2>&1
     rc=$?
     echo "pmc $c rc=$rc" >> gpurun_out/pmc_bench_$c.log
     if [ $rc -ne 0 ]; then exit $rc; fi
