@@ -76,7 +76,7 @@ struct Epi {
   int gelu_filter;           // EPI_GELU: constants are the ViT GELU's (sqrt2, 1, 0.5)
   float rsf[3], zpf[3];      // f32 RN(1/s_out), zp_out per group, for the rounding filters
   float lof, hif;            // lo, hi as f32
-  float g_rel, g_abs;        // GELU filter error terms, in units of t
+  float g_rel, g_abs, g_lim;  // GELU filter error terms, in units of t; g_lim = (0.5 - g_abs) rounded down
   int b_packed;              // Bt is the tile-packed image of nqk_pack_b
   const int32_t* colterm;    // int32 col * zpa (k_proj), or null
 };
@@ -224,6 +224,10 @@ __device__ __forceinline__ float dequant_elem(int32_t acc, int64_t colterm, floa
 // |tf| 2^-22.4): decided by tf when the rounding boundary is farther than |tf| 2^-21 (zp is
 // an integer, so zp + t rounds like t away from ties, and clipping to the integer bounds
 // commutes with rounding); else *slow is set and the caller recomputes exactly
+// quant_filter's decision room > |tf| 2^-21 + 2^-126 as |tf - r| + |tf| 2^-21 < Q_LIM in one
+// fma: Q_LIM = (0.5 - 2^-126)(1 - 2^-23) rounded down, so a rounded-down sum that passes
+// means the exact sum passes too
+constexpr float Q_LIM = 0x1.fffffcp-2f;
 __device__ __forceinline__ int quant_filter(float tf, float zpf, float lof, float hif, bool* slow) {
   const float r = __builtin_rintf(tf);
   const float room = 0.5f - __builtin_fabsf(tf - r);
@@ -262,7 +266,9 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
         // rounding boundary of t (zp is an integer, so zp + t rounds like t away from
         // ties), rint(zp + t) is decided by the cheap value; all other elements (|v| >=
         // 2^24, NaN, |h| >= 2^64) take the exact chain in a wave-uniform branch.
-        int q[4];
+        // the byte of q = clamp(rint(tf) + zp) straight from v_cvt_pk_u8_f32(q + 128)
+        // (q + 128 in [0, 255]; ^ 0x80 per byte afterwards gives two's complement)
+        const float zp128 = c.zpf + 128.0f, lo128 = e.lof + 128.0f, hi128 = e.hif + 128.0f;
         bool slow[4], any_slow = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -273,30 +279,31 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
           const float hf = c.bias[k] + df;
           const float tf = gelu_fast(hf) * c.rsf;
           const float r = __builtin_rintf(tf);
-          const float room = 0.5f - __builtin_fabsf(tf - r);
           if constexpr (F32X) {
             // g_rel also covers the product's |tf| 2^-22 (|gelu(h)| <= |h|), and
-            // |s_out| <= 2^20 makes err > 0.5 for every |h| >= 2^64 (host)
-            slow[k] = !(room > __builtin_fmaf(__builtin_fabsf(hf), e.g_rel, e.g_abs));
+            // |s_out| <= 2^20 makes err > 0.5 for every |h| >= 2^64 (host); the test
+            // |tf - r| + err < 0.5 in one fma (g_lim: 0.5 - g_abs, rounded down by 2^-23)
+            slow[k] = !(__builtin_fmaf(__builtin_fabsf(hf), e.g_rel, __builtin_fabsf(tf - r)) < e.g_lim);
           } else {
+            const float room = 0.5f - __builtin_fabsf(tf - r);
             const float err = __builtin_fmaf(__builtin_fabsf(hf), e.g_rel, e.g_abs) + __builtin_fabsf(tf) * 0x1p-22f;
             slow[k] = !((room > err) & (err < 0.25f) & (__builtin_fabsf(hf) < 0x1p64f) &
                         (vi < (1 << 24)) & (vi > -(1 << 24)));
           }
           any_slow |= slow[k];
-          q[k] = (int)__builtin_amdgcn_fmed3f(r + c.zpf, e.lof, e.hif);
+          packed = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, lo128, hi128), k, packed);
         }
+        packed ^= 0x80808080u;
         if (__builtin_expect(__any(any_slow), 0)) {
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (slow[k]) {
               const float h = c.bias[k] + dequant_elem<I32>(a[k], c.colterm[k], c.s_acc);
               const float aa = ref_erf(div_rc_u(h, e.div, e.rdiv)) + e.add1;
-              q[k] = quant_zp_u((h * aa) * e.mul2, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+              const int q = quant_zp_u((h * aa) * e.mul2, c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+              packed = (packed & ~(0xffu << (8 * k))) | ((uint32_t)(q & 0xff) << (8 * k));
             }
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) packed |= ((uint32_t)(q[k] & 0xff)) << (8 * k);
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -306,23 +313,29 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
           packed |= ((uint32_t)(q & 0xff)) << (8 * k);
         }
       }
-    } else if constexpr (F32X) {  // EPI_QKV, f32 with the rounding filter
-      int q[4];
+    } else if constexpr (F32X) {  // EPI_QKV, f32 with the rounding filter (quant_filter's
+      // test in one fma, bytes by v_cvt_pk_u8_f32 as for GELU)
+      const float zp128 = c.zpf + 128.0f, lo128 = e.lof + 128.0f, hi128 = e.hif + 128.0f;
       float y[4];
       bool slow[4], any_slow = false;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         y[k] = c.bias[k] + (float)(a[k] - (int32_t)c.colterm[k]) * c.s_acc;
-        q[k] = quant_filter(y[k] * c.rsf, c.zpf, e.lof, e.hif, &slow[k]);
+        const float tf = y[k] * c.rsf;
+        const float r = __builtin_rintf(tf);
+        slow[k] = !(__builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, __builtin_fabsf(tf - r)) < Q_LIM);
         any_slow |= slow[k];
+        packed = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, lo128, hi128), k, packed);
       }
+      packed ^= 0x80808080u;
       if (__builtin_expect(__any(any_slow), 0)) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          if (slow[k]) q[k] = quant_zp_u(y[k], c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+          if (slow[k]) {
+            const int q = quant_zp_u(y[k], c.s_out, c.rs_out, c.zp, e.lo, e.hi);
+            packed = (packed & ~(0xffu << (8 * k))) | ((uint32_t)(q & 0xff) << (8 * k));
+          }
       }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) packed |= ((uint32_t)(q[k] & 0xff)) << (8 * k);
     } else {  // EPI_QKV
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -989,34 +1002,38 @@ __device__ __forceinline__ void p2_quant(const Epi& e, const int (&a)[NG][4], co
                                          const v4i (&bs)[NG], float sacc, float rsf, float zpf, float s_out,
                                          double rs_out, double zp, uint32_t (&packed)[NG]) {
   constexpr int E = 4 * NG;
-  int q[E];
+  // bytes as in epi_row4: v_cvt_pk_u8_f32(q + 128), ^ 0x80 per byte; the filters' tests
+  // in one fma each (Q_LIM / g_lim)
+  const float zp128 = zpf + 128.0f, lo128 = e.lof + 128.0f, hi128 = e.hif + 128.0f;
   float hv[E];
   bool slow[E];
   bool any = false;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) packed[g] = 0;
 #pragma unroll
   for (int x = 0; x < E; ++x) {
     const int v = (a[x >> 2][x & 3] >> ASH) - ct[x >> 2][x & 3];
     const float h = __int_as_float(bs[x >> 2][x & 3]) + (float)v * sacc;  // the f64 dequantize, exactly (F32X)
     hv[x] = h;
     if constexpr ((NQK_PJ_DIAG & 2) != 0) {
-      q[x] = v;
+      packed[x >> 2] = __builtin_amdgcn_cvt_pk_u8_f32((float)(v & 255), x & 3, packed[x >> 2]);
       slow[x] = false;
       continue;
     }
-    float tf, thr;
-    if constexpr (EPI == EPI_GELU) {
-      tf = gelu_fast(h) * rsf;
-      thr = __builtin_fmaf(__builtin_fabsf(h), e.g_rel, e.g_abs);
-    } else {
-      tf = h * rsf;
-      thr = __builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, 0x1p-126f);
-    }
+    float tf;
+    if constexpr (EPI == EPI_GELU) tf = gelu_fast(h) * rsf;
+    else tf = h * rsf;
     const float r = __builtin_rintf(tf);
-    const float room = 0.5f - __builtin_fabsf(tf - r);
-    slow[x] = !(room > thr);
+    if constexpr (EPI == EPI_GELU)
+      slow[x] = !(__builtin_fmaf(__builtin_fabsf(h), e.g_rel, __builtin_fabsf(tf - r)) < e.g_lim);
+    else
+      slow[x] = !(__builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, __builtin_fabsf(tf - r)) < Q_LIM);
     any |= slow[x];
-    q[x] = (int)__builtin_amdgcn_fmed3f(r + zpf, e.lof, e.hif);
+    packed[x >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, lo128, hi128), x & 3,
+                                                    packed[x >> 2]);
   }
+#pragma unroll
+  for (int g = 0; g < NG; ++g) packed[g] ^= 0x80808080u;
   if (__builtin_expect(__any(any), 0)) {
 #pragma unroll
     for (int x = 0; x < E; ++x) {
@@ -1027,15 +1044,12 @@ __device__ __forceinline__ void p2_quant(const Epi& e, const int (&a)[NG][4], co
             const float aa = ref_erf(div_rc_u(y, e.div, e.rdiv)) + e.add1;
             y = (y * aa) * e.mul2;
           }
-          q[x] = quant_zp_u(y, s_out, rs_out, zp, e.lo, e.hi);
+          const int q = quant_zp_u(y, s_out, rs_out, zp, e.lo, e.hi);
+          packed[x >> 2] = (packed[x >> 2] & ~(0xffu << (8 * (x & 3)))) | ((uint32_t)(q & 0xff) << (8 * (x & 3)));
         }
       }
     }
   }
-#pragma unroll
-  for (int g = 0; g < NG; ++g)
-    packed[g] = ((uint32_t)q[4 * g] & 0xffu) | (((uint32_t)q[4 * g + 1] & 0xffu) << 8) |
-                (((uint32_t)q[4 * g + 2] & 0xffu) << 16) | ((uint32_t)q[4 * g + 3] << 24);
 }
 
 template <int EPI, bool F32X, int NK, bool B4>
@@ -1807,6 +1821,10 @@ static Epi make_epi(const nqk_epilogue* p) {
   const double ars = __builtin_fabs(1.0 / (double)p->s_out[0]) * 1.02;
   e.g_rel = (float)((double)GELU_REL * 1.27 * ars);
   e.g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
+  // |tf - r| + |h| g_rel + g_abs < 0.5 tested as RN(|h| g_rel + |tf - r|) < g_lim: a
+  // rounded-down sum below g_lim = (0.5 - g_abs)(1 - 2^-22) keeps the exact one below
+  // 0.5 - g_abs
+  e.g_lim = (float)((0.5 - (double)e.g_abs) * (1.0 - 0x1p-22));
   e.b_packed = p->b_packed;
   e.colterm = p->colterm;
   e.lof = (float)e.lo;
