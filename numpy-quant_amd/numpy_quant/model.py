@@ -73,6 +73,25 @@ class QuantizationParams:
         return f"QuantizationParams(scale={self.scale}, zero_point={self.zero_point})"
 
 
+def _listing(kind: str, fields) -> str:
+    """Readable multi-line dump of an IR object: one line per element of each list or
+    dict field (the reference prints its models this way, model.py:223-234, 464-484)."""
+    out = [f"{kind}("]
+    for name, val in fields:
+        if isinstance(val, dict):
+            out.append(f"  {name}={{")
+            out.extend(f"    {k}: {v}," for k, v in val.items())
+            out.append("  },")
+        elif isinstance(val, list):
+            out.append(f"  {name}=[")
+            out.extend(f"    {e}" for e in val)
+            out.append("  ],")
+        else:
+            out.append(f"  {name}={val},")
+    out.append(")")
+    return "\n".join(out) + "\n"
+
+
 # ----------------------------------------------------------------------------- operators
 def _gemm(inputs, attrs):
     x, w, b = inputs
@@ -167,19 +186,11 @@ class Model:
         self.outputs = outputs
 
     def __repr__(self):
-        return f"Model(nodes={self.nodes}, values={self.values}, inputs={self.inputs}, outputs={self.values})"
+        return f"Model({len(self.nodes)} nodes, {len(self.values)} values, inputs={self.inputs}, outputs={self.outputs})"
 
     def __str__(self):
-        res = "Model(\n"
-        for k, v in self.__dict__.items():
-            if not isinstance(v, list):
-                continue
-            res += f"  {k}=[\n"
-            for e in v:
-                res += f"    {e}\n"
-            res += "  ],\n"
-        res += ")\n"
-        return res
+        return _listing("Model", [("nodes", self.nodes), ("values", self.values), ("inputs", self.inputs),
+                                  ("outputs", self.outputs)])
 
     def __del__(self):
         # break node <-> value cycles so device buffers are released promptly (model.py:236-247)
@@ -396,28 +407,13 @@ class QModel(Model):
         self.keep_values = False
 
     def __repr__(self):
-        return (f"QModel(nodes={self.nodes}, values={self.values}, inputs={self.inputs}, outputs={self.values}, "
-                f"bit_width={self.bit_width}, quant_params={self.quant_params})")
+        return (f"QModel({len(self.nodes)} nodes, {len(self.values)} values, bit_width={self.bit_width}, "
+                f"inputs={self.inputs}, outputs={self.outputs})")
 
     def __str__(self):
-        res = "QModel(\n"
-        for k, v in self.__dict__.items():
-            if k.startswith("_"):
-                continue
-            if isinstance(v, list):
-                res += f"  {k}=[\n"
-                for e in v:
-                    res += f"    {e}\n"
-                res += "  ],\n"
-            if isinstance(v, dict):
-                res += f"  {k}={{\n"
-                for ek, ev in v.items():
-                    res += f"    {ek}: {ev},\n"
-                res += "  }},\n"
-            else:
-                res += f"  {k}={v},\n"
-        res += ")\n"
-        return res
+        return _listing("QModel", [("nodes", self.nodes), ("values", self.values), ("inputs", self.inputs),
+                                   ("outputs", self.outputs), ("bit_width", self.bit_width),
+                                   ("quant_params", self.quant_params)])
 
     def _dequant_input(self, value: Value) -> FTensor:
         if isinstance(value, Constant):
