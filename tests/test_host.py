@@ -144,3 +144,38 @@ def test_blas_order_matches_numpy_matmul(K):
     rows, cols = np.arange(0, 40, 5), np.arange(0, 64, 9)
     got = _fma_chain_blocks(A[rows].astype(np.float64), W[:, cols].astype(np.float64), K)
     np.testing.assert_array_equal(got.astype(np.float32), C[np.ix_(rows, cols)])
+
+
+def _proto_view(m):
+    """onnx_proto's decode in _onnx_walk's shape."""
+    def val(a):
+        if a.type == onnx_proto.ATTR_TENSOR:
+            return ("tensor", tuple(a.t.dims), a.t.data_type)
+        v = onnx_proto.attribute_value(a)
+        if isinstance(v, bytes):
+            return v.decode()
+        if isinstance(v, list):
+            return tuple(v)
+        return v
+    g = m.graph
+    nodes = [(n.name, n.op_type, tuple(n.input), tuple(n.output), {a.name: val(a) for a in n.attribute}) for n in g.node]
+    inits = [(t.name, tuple(t.dims), t.data_type) for t in g.initializer]
+    return nodes, inits, [v.name for v in g.input], [v.name for v in g.output]
+
+
+@pytest.mark.parametrize("fname", ["mlp.onnx", "vit_image_classifier_no_weights.onnx",
+                                   "vit_image_classifier_encoder_layer_no_weights.onnx",
+                                   "vit_image_classifier_self_attention_no_weights.onnx"])
+def test_onnx_decode_matches_independent_reader(fname):
+    """The product's ONNX decoder against a separately written wire-format reader
+    (tests/_onnx_walk.py) on every graph the fixtures use: every node's name, op type,
+    inputs, outputs and attribute values, every initializer's name, shape and element
+    type, the graph inputs and outputs (the fixtures and the product
+    share onnx_proto, so it needs a pin of its own)."""
+    import _onnx_walk
+    path = os.path.join(MODELS, fname)
+    want = _onnx_walk.read(path)
+    got = _proto_view(onnx_proto.load(path, synthetic_weights="no_weights" in fname))
+    assert got[0] == want[0]
+    assert got[1] == want[1]
+    assert got[2] == want[2] and got[3] == want[3]
