@@ -146,6 +146,15 @@ int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch, int64_t M
               int64_t K, int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc,
               const int64_t* bmap, int64_t a_mat_stride, int64_t b_mat_stride, int64_t c_mat_stride);
 
+/* One-row float product y[N] = x[1][K] . B[K][N] where B's columns are contiguous
+ * (bt[N][ldb], the layout of the Gemm's w.T view, model.py:122-131): NumPy's matmul hands
+ * that to OpenBLAS's GEMV-T (vector_matrix -> cblas_sgemv), and this reproduces its order
+ * bit for bit — the N columns split over `threads` chunks as OpenBLAS's gemv threading does
+ * (one chunk when K*N < 460800), 8-lane fma / 4-lane SSE kernels per column class, K blocks
+ * of 4096, trailing rows (oracle/openblas_order.py).  `threads` = OpenBLAS's thread count
+ * of the NumPy being matched. */
+int nqk_sgemv_t(const float* x, const float* bt, float* y, int64_t N, int64_t K, int64_t ldb, int64_t threads);
+
 /* im2col for Conv (numpy_helper.py:18-70): x NCHW f32 -> cols[N*Ho*Wo][KH*KW*C]
  * (column order kh, kw, c), zero padding pads = (ph0, pw0, ph1, pw1). */
 /* ViT patch embedding in one GEMM (plan.py FusedEmbed): Conv as im2col . W in the BLAS

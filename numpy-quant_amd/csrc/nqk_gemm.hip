@@ -437,6 +437,98 @@ __global__ void k_im2col(const float* __restrict__ x, float* __restrict__ cols, 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// One-row float product y = x[1][K] . B[K][N] with B's columns contiguous (Bt[N][K]): NumPy
+// hands it to OpenBLAS's GEMV-T (matmul.cpp vector_matrix -> cblas_sgemv(ColMajor, Trans)),
+// whose order this kernel reproduces (oracle/openblas_order.py states it and pins it to
+// np.matmul): the N columns split over `threads` chunks (gemv_thread.c); per chunk, groups
+// of 4 columns by the AVX2 4x4 kernel (8 fma lanes), 2 leftover columns by the SSE 4x2
+// kernel (4 mul+add lanes), 1 by the SSE 4x1 kernel (2 x 4 mul+add lanes); K in blocks of
+// 4096 added to y in order; K % 4 trailing rows in scalar C with fma contraction.
+// Eight lanes per column (one per accumulator lane of the CPU kernel), 8 columns per wave.
+__device__ __forceinline__ int gemv_class(int64_t j, int64_t N, int threads) {
+  // chunk [j0, j1) of column j: widths ceil(rem / threads left), at least 4
+  int64_t j0 = 0, rem = N;
+  for (int t = 0; rem > 0; ++t) {
+    int64_t w = threads - t > 0 ? (rem + threads - t - 1) / (threads - t) : rem;
+    w = w < 4 ? 4 : w;
+    w = w > rem ? rem : w;
+    if (j < j0 + w) {
+      const int64_t n = w, n4 = n & ~(int64_t)3, loc = j - j0;
+      if (loc < n4) return 0;              // 4x4
+      if (((n - n4) & 2) && loc < n4 + 2) return 1;  // 4x2
+      return 2;                            // 4x1
+    }
+    j0 += w;
+    rem -= w;
+  }
+  return 0;
+}
+
+__global__ void __launch_bounds__(256)
+k_sgemv_t(const float* __restrict__ x, const float* __restrict__ bt, float* __restrict__ y, int64_t N, int64_t K,
+          int64_t ldb, int threads) {
+  const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+  const int l = threadIdx.x & 7;
+  const bool live = j < N;
+  const int64_t jj = live ? j : N - 1;
+  const float* col = bt + jj * ldb;
+  const int cls = gemv_class(jj, N, threads);
+  const int64_t m3 = K & 3;
+  int64_t m1 = K & ~(int64_t)3;
+  const int64_t m2 = (K & 4095) - m3;
+  float yv = 0.0f;
+  int64_t k0 = 0, nb = 4096;
+  while (nb == 4096) {
+    m1 -= nb;
+    if (m1 < 0) {
+      if (m2 == 0) break;
+      nb = m2;
+    }
+    const float* a = col + k0;
+    const float* xb = x + k0;
+    float acc = 0.0f;
+    int64_t i = 0;
+    if (cls == 0) {  // lane l: an fma chain over rows l, l + 8, ... (after a 4-row prologue)
+      if (nb & 4) {
+        if (l < 4) acc = __builtin_fmaf(xb[l], a[l], acc);
+        i = 4;
+      }
+      for (; i < nb; i += 8) acc = __builtin_fmaf(xb[i + l], a[i + l], acc);
+    } else if (cls == 1) {  // lanes 0-3: rows r = l mod 4, multiply then add
+      if (l < 4)
+        for (; i < nb; i += 4) acc = acc + xb[i + l] * a[i + l];
+    } else {  // lane l: set l / 4, row l % 4 of each 8-row step (prologue rows to set 0)
+      if (nb & 4) {
+        if (l < 4) acc = acc + xb[l] * a[l];
+        i = 4;
+      }
+      for (; i < nb; i += 8) acc = acc + xb[i + l] * a[i + l];
+    }
+    // lanes (r + r+4), then ((0+1) + (2+3)); the 4x2 kernel has no upper lanes
+    const float up = __shfl_down(acc, 4, 8);
+    const float h = cls == 1 ? acc : acc + up;
+    const float h1 = __shfl_down(h, 1, 8);
+    const float p = h + h1;  // lanes 0 and 2: (h0 + h1), (h2 + h3)
+    const float p2 = __shfl_down(p, 2, 8);
+    const float s = p + p2;  // lane 0
+    yv = yv + s;
+    k0 += nb;
+  }
+  if (m3) {
+    const float* a = col + k0;
+    const float* xb = x + k0;
+    if (m3 == 1) {
+      yv = __builtin_fmaf(a[0], xb[0], yv);
+    } else {
+      float t = __builtin_fmaf(a[0], xb[0], a[1] * xb[1]);
+      if (m3 == 3) t = __builtin_fmaf(a[2], xb[2], t);
+      yv = yv + t;
+    }
+  }
+  if (live && l == 0) y[j] = yv;
+}
+
 }  // namespace
 
 // OpenBLAS level-3 K blocking (driver/level3/level3.c): GEMM_Q = 448 for SkylakeX sgemm
@@ -572,4 +664,17 @@ extern "C" int nqk_im2col(const float* x, float* cols, int64_t n, int64_t c, int
   hipLaunchKernelGGL(k_im2col, dim3(grid_for(total)), dim3(kThreads), 0, stream(), x, cols, n, c, h, w, kh, kw, ph0,
                      pw0, sh, sw, ho, wo);
   return launch_status("nqk_im2col");
+}
+
+extern "C" int nqk_sgemv_t(const float* x, const float* bt, float* y, int64_t N, int64_t K, int64_t ldb,
+                           int64_t threads) {
+  if (N <= 0) return 0;
+  if (K <= 0) return fail("nqk_sgemv_t: K >= 1 expected");
+  if (ldb < K) return fail("nqk_sgemv_t: ldb < K");
+  if (threads < 1 || threads > 1024) return fail("nqk_sgemv_t: 1 <= threads <= 1024 expected");
+  // interface/gemv.c: one thread below m * n = 115200 * GEMM_MULTITHREAD_THRESHOLD (4)
+  const int t = (K * N < 115200 * 4) ? 1 : (int)threads;
+  const int64_t lanes = N * 8;
+  hipLaunchKernelGGL(k_sgemv_t, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream(), x, bt, y, N, K, ldb, t);
+  return launch_status("nqk_sgemv_t");
 }

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 
@@ -309,6 +310,46 @@ def sgemm(a: DeviceArray, a_sm, a_sk, b: DeviceArray, b_sk, b_sn, M, N, K, batch
     _lib.call("nqk_sgemm", a.vp, b.vp, c.vp, batch, M, N, K, a_sm, a_sk, b_sk, b_sn, N,
               _lib.i64arr(bmap) if bmap is not None else None, a_ms, b_ms, M * N)
     return c
+
+
+# OpenBLAS thread count of the NumPy whose GEMV order is reproduced (its column split
+# depends on it, oracle/openblas_order.py): NQK_BLAS_THREADS, else what OpenBLAS itself
+# reads (OPENBLAS_NUM_THREADS, GOTO_NUM_THREADS, OMP_NUM_THREADS, else the CPUs this
+# process may run on), at most 64 (scipy-openblas MAX_THREADS)
+BLAS_THREADS = None
+
+
+def openblas_threads() -> int:
+    if BLAS_THREADS is not None:
+        return int(BLAS_THREADS)
+    for v in ("NQK_BLAS_THREADS", "OPENBLAS_NUM_THREADS", "GOTO_NUM_THREADS", "OMP_NUM_THREADS"):
+        s = os.environ.get(v, "").strip()
+        if s.isdigit() and int(s) > 0:
+            return min(int(s), 64)
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 64))
+
+
+def gemv_t_applies(M: int, N: int, K: int) -> bool:
+    """NumPy sends a one-row product x[1, K] @ B[K, N] (N > 1) whose B has unit stride
+    along K to OpenBLAS GEMV-T; nqk_sgemv_t reproduces its order for K >= 9 and K = 1, 4
+    (pinned against np.matmul; K in 2..8 other than 4 takes special small-matrix paths
+    there that are not restated)."""
+    return M == 1 and N > 1 and (K >= 9 or K in (1, 4))
+
+
+def sgemv_t(x: DeviceArray, bt: DeviceArray) -> DeviceArray:
+    """y[1, N] = x[1, K] . bt[N, K]^T in OpenBLAS GEMV-T order (nqk_sgemv_t)."""
+    N, Kb = bt.shape
+    K = x.shape[-1]
+    if Kb != K or x.size != K:
+        raise ValueError(f"matmul: mismatch in core dimension ({K} vs {Kb})")
+    y = DeviceArray((1, N), np.float32)
+    _lib.call("nqk_sgemv_t", x.vp, bt.vp, y.vp, N, K, K, openblas_threads())
+    return y
 
 
 def matmul_f32(a: DeviceArray, b: DeviceArray) -> DeviceArray:

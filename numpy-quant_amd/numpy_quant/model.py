@@ -98,6 +98,11 @@ def _gemm(inputs, attrs):
     if attrs.get("transA"):
         x = x.T
     if attrs.get("transB"):
+        if (isinstance(x, FTensor) and isinstance(w, FTensor) and x.dev.ndim == 2 and w.dev.ndim == 2
+                and K.gemv_t_applies(x.dev.shape[0], w.dev.shape[0], x.dev.shape[1])):
+            # x[1, K] @ w.T: NumPy's matmul takes OpenBLAS GEMV-T for this layout (the
+            # w.T view has its columns contiguous), whose summation order differs from GEMM's
+            return [FTensor(K.sgemv_t(x.dev, w.dev)) + b]
         w = w.T
     return [x.matmul(w) + b]
 

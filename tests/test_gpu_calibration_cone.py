@@ -1,25 +1,21 @@
-"""The calibration cone, bounded.
+"""The calibration cone, now closed on the reference's fixtures.
 
 Model.quantize (reference model.py:328-442) calibrates on a float forward whose MatMuls
-are OpenBLAS np.matmul (reference tensor.py:100-101).  The device float forward
-(nqk_sgemm: OpenBLAS's GEMM_Q = 448 K blocks, k-ordered fma chains) equals it bit for
-bit for every GEMM with more than one row, any K.  A one-row product (the classifier
-Gemm on the CLS token) runs in OpenBLAS as sgemv, whose order is not reproduced, so
-the values downstream of it (the "cone", tests/test_gpu_models.py:tainted_values) may
-differ by ulps, and so may the quantization parameters calibrated on them.  This test
-bounds that gap on the reference's own fixtures (tests/golden/vit_b1 and layer_b1,
-recorded from the reference):
+are OpenBLAS np.matmul (reference tensor.py:100-101).  The device float forward equals
+it bit for bit: every GEMM with more than one row through nqk_sgemm (OpenBLAS's
+GEMM_Q = 448 K blocks, k-ordered fma chains), and the one-row classifier Gemm on the CLS
+token through nqk_sgemv_t (OpenBLAS's GEMV-T order, oracle/openblas_order.py, with the
+fixtures' 8-thread column split, tests/conftest.py).  Values downstream of one-row
+products whose order is not restated (tests/test_gpu_models.py:tainted_values) form the
+"cone"; for the fixtures below it is empty, so this test asserts:
 
-  * every scale outside the cone is bit-identical, and inside it at most SCALE_ULPS
-    float32 ulps from the reference's;
-  * every zero point inside the cone within 1 of the reference's;
-  * the output of the device-calibrated QModel on the reference's run input against the
-    reference's output (both dequantized float32) within north_star's 1e-5.
+  * every scale and zero point bit-identical to the reference's (the SCALE_ULPS / |dzp|
+    bounds remain the contract for a non-empty cone);
+  * the device-calibrated QModel's output on the reference's run input equal to the
+    reference's output, bit for bit (north_star's 1e-5 bound for a non-empty cone).
 
-Measured on MI355X: layer_b1 has an empty cone (bit-identical); vit_b1 one parameter
-(the logits' scale, 4 ulps), logits within 4.8e-7.  (With GEMM_Q = 384, as in round 1,
-the K = 3072 FFN-down MatMuls joined the cone: 318 of 438 scales off by up to 8 ulps
-and 58.5 % of the logits off by 1-3 output steps.)"""
+History: round 1 (GEMM_Q = 384, no GEMV order) had 318 of 438 vit_b1 scales off by up to
+8 ulps; GEMM_Q = 448 left one (the logits' scale, 4 ulps, from the classifier's GEMV)."""
 import json
 import os
 
@@ -75,6 +71,8 @@ def test_calibration_cone_is_bounded(tag, fname):
     print(msg)
     assert max(ulps, default=0) <= SCALE_ULPS, msg
     assert max(dzp, default=0) <= 1, msg
+    assert not taint, f"{tag}: one-row products outside the restated GEMV order: {sorted(taint)[:8]}"
+    assert n_scale == 0 and n_zp == 0, msg
     out = np.asarray(qmodel([arrs["x_run"]])[0], dtype=np.float32)
     want = np.asarray(arrs[f"{bw_key}_out"], dtype=np.float32)
     assert out.shape == want.shape
@@ -82,3 +80,4 @@ def test_calibration_cone_is_bounded(tag, fname):
     msg2 = f"{tag}: output |diff| max {diff.max():.3g}, {float(np.mean(diff > 0)):.2%} of {diff.size} elements differ"
     print(msg2)
     assert diff.max() <= OUT_ATOL, msg2
+    np.testing.assert_array_equal(out, want)

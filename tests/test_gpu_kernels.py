@@ -174,3 +174,43 @@ def test_sgemm_mfma_equals_fma_chain_kernel(batch, M, N, K, monkeypatch):
     monkeypatch.setenv("NQK_SGEMM_VALU", "1")
     ref = KM.sgemm(a, K, 1, b, N, 1, M, N, K, batch=batch, bmap=bmap, a_ms=M * K, b_ms=K * N).to_host()
     np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("K,N,threads", [(768, 1000, 8), (768, 1000, 3), (768, 1000, 16), (772, 1001, 8),
+                                         (780, 2001, 8), (770, 1000, 4), (771, 37, 1), (5000, 30, 1),
+                                         (8200, 17, 1), (4100, 130, 8), (9, 300, 1), (4, 2304, 1), (1, 50, 1),
+                                         (3072, 300, 64)])
+def test_sgemv_t_matches_openblas_order(K, N, threads):
+    """nqk_sgemv_t (one-row float product against a transposed weight: the reference's
+    classifier Gemm at batch 1, model.py:122-131 -> np.matmul -> OpenBLAS GEMV-T) equals
+    the oracle's restatement of OpenBLAS's order (oracle/openblas_order.py, pinned to
+    np.matmul by tests/test_host.py) bit for bit, at several OpenBLAS thread counts."""
+    from numpy_quant import kernels as KM
+    from numpy_quant.device import DeviceArray
+    from oracle.openblas_order import sgemv_t
+    rng = np.random.default_rng(K + 3 * N)
+    x = rng.standard_normal(K).astype(np.float32)
+    w = (0.05 * rng.standard_normal((N, K))).astype(np.float32)
+    old = KM.BLAS_THREADS
+    KM.BLAS_THREADS = threads
+    try:
+        got = KM.sgemv_t(DeviceArray.from_host(x[None, :]), DeviceArray.from_host(w)).to_host()[0]
+    finally:
+        KM.BLAS_THREADS = old
+    want = sgemv_t(w, x, threads)
+    np.testing.assert_array_equal(got.view(np.int32), want.view(np.int32))
+
+
+def test_one_row_gemm_takes_gemv_order():
+    """Model-level: a float Gemm(transB=1) on one row (model.py:122-131) goes through the
+    GEMV-T order, a two-row one through the GEMM order: both bit-exact vs the oracle's
+    restatements of what NumPy does there."""
+    from numpy_quant.model import onnx_operator_implementation
+    from numpy_quant.tensor import FTensor
+    from oracle.openblas_order import sgemv_t
+    rng = np.random.default_rng(5)
+    w = (0.05 * rng.standard_normal((1000, 768))).astype(np.float32)
+    b = rng.standard_normal(1000).astype(np.float32)
+    x1 = rng.standard_normal((1, 768)).astype(np.float32)
+    y1 = onnx_operator_implementation("Gemm", [FTensor(x1), FTensor(w), FTensor(b)], {"transB": 1})[0].data
+    np.testing.assert_array_equal(y1, (sgemv_t(w, x1[0], 8) + b)[None, :])

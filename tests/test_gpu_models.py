@@ -93,20 +93,24 @@ def ref_qparams(meta_qp):
 
 
 def tainted_values(model):
-    """Values downstream of a float MatMul/Gemm with one row (M = 1): OpenBLAS runs
-    those as sgemv, whose summation order nqk_sgemm does not reproduce,
-    so the float calibration forward is bit-exact everywhere else and ulp-close there.
-    (Every GEMM with M > 1, any K, is reproduced: OpenBLAS's GEMM_Q = 448 K blocks.)"""
+    """Values downstream of a float one-row product (M = 1) whose OpenBLAS order is not
+    reproduced: a one-row Gemm against a transposed weight goes to OpenBLAS GEMV-T, which
+    nqk_sgemv_t reproduces (oracle/openblas_order.py; K >= 9); other one-row products
+    (GEMV-N, dot, tiny K) are not restated, so values downstream of them may differ by
+    ulps.  Every GEMM with M > 1, any K, is reproduced (OpenBLAS's GEMM_Q = 448 K blocks)."""
+    from numpy_quant.kernels import gemv_t_applies
     bad = set()
     for node in model.nodes:
         ins = [i.name for i in node.inputs]
         if node.op in ("MatMul", "Gemm"):
             a = node.inputs[0].data
-            k = a.dev.shape[-1] if hasattr(a, "dev") else 0
-            if node.op == "Gemm" and node.attrs.get("transA"):
-                k = a.dev.shape[-2]
+            w = node.inputs[1].data
             if a.dev.ndim >= 2 and a.dev.shape[-2] == 1:
-                bad.update(o.name for o in node.outputs)
+                covered = (node.op == "Gemm" and node.attrs.get("transB") and not node.attrs.get("transA")
+                           and a.dev.ndim == 2 and w.dev.ndim == 2
+                           and gemv_t_applies(1, w.dev.shape[0], a.dev.shape[1]))
+                if not covered:
+                    bad.update(o.name for o in node.outputs)
         if any(i in bad for i in ins):
             bad.update(o.name for o in node.outputs)
             # constants quantized with a tainted value's scale (Gemm / Add biases at 4*bw)
@@ -144,7 +148,7 @@ def test_vit_graphs_bit_exact(tag, fname, batch):
                 kind, arr = _canon(v.data)
                 if hashlib.sha256(arr.tobytes()).hexdigest() != meta["float_hashes"][v.name][2]:
                     fbad.append(v.name)
-            assert set(fbad) <= taint, f"float values differing outside the K>768 cone: {sorted(set(fbad) - taint)[:8]}"
+            assert set(fbad) <= taint, f"float values differing outside the one-row cone: {sorted(set(fbad) - taint)[:8]}"
         qbad = _check_qparams(qmodel.quant_params, meta[bw_key]["qparams"], strict=False)
         assert set(qbad) <= taint, sorted(set(qbad) - taint)[:8]
         if not taint:

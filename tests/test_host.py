@@ -179,3 +179,28 @@ def test_onnx_decode_matches_independent_reader(fname):
     assert got[0] == want[0]
     assert got[1] == want[1]
     assert got[2] == want[2] and got[3] == want[3]
+
+
+_GEMV_CASES = [(768, 1000, 8), (768, 1000, 3), (768, 1000, 4), (768, 1001, 8), (772, 1001, 8), (780, 2001, 8),
+               (770, 1000, 8), (771, 37, 1), (769, 60, 1), (5000, 30, 1), (8200, 17, 1), (4100, 130, 8),
+               (100, 90, 1), (9, 300, 1), (12, 64, 1), (4, 2304, 1), (1, 50, 1), (3072, 300, 8), (256, 2001, 8)]
+
+
+@pytest.mark.parametrize("K,N,threads", _GEMV_CASES)
+def test_sgemv_order_matches_numpy_matmul(K, N, threads):
+    """oracle/openblas_order.py (OpenBLAS 0.3.29 GEMV-T: thread split of the columns, the
+    4x4 / 4x2 / 4x1 kernels' lane orders, K blocks, trailing rows) equals np.matmul of a
+    one-row product against a transposed weight, the reference's classifier Gemm at batch
+    1 (model.py:122-131), bit for bit, at OpenBLAS thread counts 1..8.  Skipped where
+    OpenBLAS runs other kernel families."""
+    threadpoolctl = pytest.importorskip("threadpoolctl")
+    info = [i for i in threadpoolctl.threadpool_info() if i.get("internal_api") == "openblas"]
+    if not info or info[0].get("architecture") not in ("Haswell", "Zen", "SkylakeX", "Cooperlake", "SapphireRapids"):
+        pytest.skip("OpenBLAS does not run its Haswell-family GEMV kernels on this host")
+    from oracle.openblas_order import sgemv_t
+    rng = np.random.default_rng(K * 7 + N)
+    x = rng.standard_normal(K).astype(np.float32)
+    w = (0.05 * rng.standard_normal((N, K))).astype(np.float32)
+    with threadpoolctl.threadpool_limits(limits=threads, user_api="blas"):
+        ref = (x[None, :] @ w.T)[0]
+    np.testing.assert_array_equal(sgemv_t(w, x, threads).view(np.int32), ref.view(np.int32))
