@@ -975,6 +975,13 @@ __device__ __forceinline__ void lgkm_wait() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+// the value of this register in the partner lane (lane ^ 32): v_permlane32_swap + a select
+__device__ __forceinline__ uint32_t pswap32(uint32_t x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (threadIdx.x & 32) ? (uint32_t)r[0] : (uint32_t)r[1];
+}
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -1005,9 +1012,22 @@ __device__ __forceinline__ void p2_quant(const Epi& e, const int (&a)[NG][4], co
   // bytes as in epi_row4: v_cvt_pk_u8_f32(q + 128), ^ 0x80 per byte; the filters' tests
   // in one fma each (Q_LIM / g_lim)
   const float zp128 = zpf + 128.0f, lo128 = e.lof + 128.0f, hi128 = e.hif + 128.0f;
+  // the filter's measure d = (distance to the rounding boundary's complement) + error bound
+  // (>= 0, or NaN); the element is decided when d < lim.  The fast path keeps only the
+  // largest d of the batch, as an unsigned max of the bit patterns (NaN and inf order
+  // above every finite), one instruction per element; a batch with any undecided element
+  // recomputes the same d per element (same operations, same values) for the exact chain
+  const float lim = EPI == EPI_GELU ? e.g_lim : Q_LIM;
+  auto measure = [&](float h, float& r) __attribute__((always_inline)) {
+    float tf;
+    if constexpr (EPI == EPI_GELU) tf = gelu_fast(h) * rsf;
+    else tf = h * rsf;
+    r = __builtin_rintf(tf);
+    if constexpr (EPI == EPI_GELU) return __builtin_fmaf(__builtin_fabsf(h), e.g_rel, __builtin_fabsf(tf - r));
+    else return __builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, __builtin_fabsf(tf - r));
+  };
   float hv[E];
-  bool slow[E];
-  bool any = false;
+  uint32_t worst = 0;
 #pragma unroll
   for (int g = 0; g < NG; ++g) packed[g] = 0;
 #pragma unroll
@@ -1017,28 +1037,23 @@ __device__ __forceinline__ void p2_quant(const Epi& e, const int (&a)[NG][4], co
     hv[x] = h;
     if constexpr ((NQK_PJ_DIAG & 2) != 0) {
       packed[x >> 2] = __builtin_amdgcn_cvt_pk_u8_f32((float)(v & 255), x & 3, packed[x >> 2]);
-      slow[x] = false;
       continue;
     }
-    float tf;
-    if constexpr (EPI == EPI_GELU) tf = gelu_fast(h) * rsf;
-    else tf = h * rsf;
-    const float r = __builtin_rintf(tf);
-    if constexpr (EPI == EPI_GELU)
-      slow[x] = !(__builtin_fmaf(__builtin_fabsf(h), e.g_rel, __builtin_fabsf(tf - r)) < e.g_lim);
-    else
-      slow[x] = !(__builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, __builtin_fabsf(tf - r)) < Q_LIM);
-    any |= slow[x];
+    float r;
+    const float d = measure(h, r);
+    worst = __builtin_elementwise_max(worst, __float_as_uint(d));
     packed[x >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, lo128, hi128), x & 3,
                                                     packed[x >> 2]);
   }
 #pragma unroll
   for (int g = 0; g < NG; ++g) packed[g] ^= 0x80808080u;
-  if (__builtin_expect(__any(any), 0)) {
+  if (__builtin_expect(__any(worst >= __float_as_uint(lim)), 0)) {
 #pragma unroll
     for (int x = 0; x < E; ++x) {
-      if (__any(slow[x])) {
-        if (slow[x]) {
+      float r;
+      const bool slow = !(measure(hv[x], r) < lim);
+      if (__any(slow)) {
+        if (slow) {
           float y = hv[x];
           if constexpr (EPI == EPI_GELU) {
             const float aa = ref_erf(div_rc_u(y, e.div, e.rdiv)) + e.add1;
@@ -1065,9 +1080,10 @@ k_proj(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N
   constexpr int RD = p2_depth(EPI);
   static_assert(NK % RD == 0 && NK >= 2 * RD, "k_proj: NK a multiple of the ring depth");
   static_assert(p2_lds(EPI, B4) <= 160 * 1024, "k_proj: LDS");
-  // VMEM operations of one epilogue: QKV / GELU 32 stores; RESID 15 x 8 residual loads +
-  // 16 x 8 stores (the counter never holds more than 63)
-  constexpr int EOPS = RESID ? 248 : 32;
+  // VMEM operations of one epilogue: QKV / GELU 8 16-byte stores; RESID 15 x 8 residual
+  // loads + 16 x 8 stores (the counter never holds more than 63).  Exact: the k loop's
+  // vmcnt waits count the epilogue's operations as younger than the prefetched stages
+  constexpr int EOPS = RESID ? 248 : 8;
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1256,11 +1272,11 @@ k_proj(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N
         for (int i = 0; i < 4; ++i) {
           const int m = r0 + wm * 128 + i * 32 + r32;
           const int img = m / e.tokens, t = m - img * e.tokens;
-          rowoff[i] = (uint32_t)(((img * e.heads + hh) * e.tokens + t) * e.hdim) + 4 * half;
+          rowoff[i] = (uint32_t)(((img * e.heads + hh) * e.tokens + t) * e.hdim) + 16 * half;
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) rowoff[i] = (uint32_t)(r0 + wm * 128 + i * 32 + r32) * (uint32_t)N + cw + 4 * half;
+        for (int i = 0; i < 4; ++i) rowoff[i] = (uint32_t)(r0 + wm * 128 + i * 32 + r32) * (uint32_t)N + cw + 16 * half;
       }
       const float sacc = g3 == 0 ? e.s_acc[0] : (g3 == 1 ? e.s_acc[1] : e.s_acc[2]);
       const float rsf = g3 == 0 ? e.rsf[0] : (g3 == 1 ? e.rsf[1] : e.rsf[2]);
@@ -1275,6 +1291,7 @@ k_proj(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N
       // the lane's 4 column groups of N-subtile j are read at its first batch
       constexpr int NG = EPI == EPI_GELU ? 2 : 4, NB = 32 / NG;
       v4i ct[4], bs[4];
+      uint32_t pk[4];  // the 4 column groups of MFMA tile (i, j), gathered over its batches
       static_for<0, NB>([&](auto BI) __attribute__((always_inline)) {
         constexpr int b = decltype(BI)::value, j = b / (NB / 2), i = (b % (NB / 2)) / (4 / NG),
                       g0 = (b % (4 / NG)) * NG;
@@ -1298,15 +1315,19 @@ k_proj(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N
         }
         uint32_t packed[NG];
         p2_quant<EPI, B4 ? 4 : 0, NG>(e, a, cg, bg, sacc, rsf, zpf, s_out, rs_out, zp, packed);
-        if constexpr ((NQK_PJ_DIAG & 1) != 0) {
-          uint32_t t = 0;
 #pragma unroll
-          for (int g = 0; g < NG; ++g) t ^= packed[g];
-          asm volatile("" ::"v"(t));
-        } else {
-#pragma unroll
-          for (int g = 0; g < NG; ++g)
-            __builtin_amdgcn_raw_buffer_store_b32(packed[g], out, rowoff[i] + j * 32 + 8 * (g0 + g), 0, 0);
+        for (int g = 0; g < NG; ++g) pk[g0 + g] = packed[g];
+        if constexpr (g0 + NG == 4) {
+          // lane (r, h) holds columns 8g + 4h .. + 3 of its row for g = 0..3; one exchange
+          // with the partner half-lane gives half 0 columns 0..15 and half 1 columns
+          // 16..31 of the tile: one 16-byte store per lane instead of four 4-byte ones
+          const uint32_t x0 = pswap32(half ? pk[0] : pk[2]), x1 = pswap32(half ? pk[1] : pk[3]);
+          const v4u st = half ? v4u{x0, pk[2], x1, pk[3]} : v4u{pk[0], x0, pk[1], x1};
+          if constexpr ((NQK_PJ_DIAG & 1) != 0) {
+            asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b128(st, out, rowoff[i] + j * 32, 0, 0);
+          }
         }
       });
     }
@@ -1906,6 +1927,7 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     const bool proj_shape = params->b_packed && i32 && params->colterm != nullptr && M >= 256 && (M % 256 == 0 || epi != EPI_RESID) && N % GBN == 0 &&
                             (K == 768 || K == 3072) && (double)M * N * 4.0 < 4294967295.0 && (double)M * lda < 4294967295.0 &&
                             !getenv("NQK_NO_PROJ") &&
+                            (epi == EPI_RESID || (al(params->out[0], 16) && al(params->out[1], 16) && al(params->out[2], 16))) &&
                             ((epi == EPI_RESID && !(params->b_packed == 2 && K == 768) && getenv("NQK_PROJ_RESID")) ||
                              (f32x && K == 768 &&
                               ((epi == EPI_GELU && getenv("NQK_PROJ_GELU")) ||
