@@ -269,32 +269,51 @@ __device__ __forceinline__ void epi_row4(const Epi& e, int gm, int img, int t, i
         // the byte of q = clamp(rint(tf) + zp) straight from v_cvt_pk_u8_f32(q + 128)
         // (q + 128 in [0, 255]; ^ 0x80 per byte afterwards gives two's complement)
         const float zp128 = c.zpf + 128.0f, lo128 = e.lof + 128.0f, hi128 = e.hif + 128.0f;
-        bool slow[4], any_slow = false;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        // the filter's decision per element; F32X keeps only the batch's largest measure
+        // as an unsigned max of its bits (measure >= 0 or NaN: NaN / inf order above every
+        // finite) and recomputes the decisions, identically, when any element may be slow
+        auto decide = [&](int k, float& r, uint32_t& m) __attribute__((always_inline)) {
           int32_t vi;
           if constexpr (I32) vi = a[k] - (int32_t)c.colterm[k];
           else vi = (int32_t)__builtin_fmin(__builtin_fmax((double)((int64_t)a[k] - c.colterm[k]), -2147483520.0), 2147483520.0);
           const float df = (float)vi * c.s_acc;
           const float hf = c.bias[k] + df;
           const float tf = gelu_fast(hf) * c.rsf;
-          const float r = __builtin_rintf(tf);
+          r = __builtin_rintf(tf);
           if constexpr (F32X) {
             // g_rel also covers the product's |tf| 2^-22 (|gelu(h)| <= |h|), and
             // |s_out| <= 2^20 makes err > 0.5 for every |h| >= 2^64 (host); the test
             // |tf - r| + err < 0.5 in one fma (g_lim: 0.5 - g_abs, rounded down by 2^-23)
-            slow[k] = !(__builtin_fmaf(__builtin_fabsf(hf), e.g_rel, __builtin_fabsf(tf - r)) < e.g_lim);
+            m = __float_as_uint(__builtin_fmaf(__builtin_fabsf(hf), e.g_rel, __builtin_fabsf(tf - r)));
+            return m >= __float_as_uint(e.g_lim);
           } else {
             const float room = 0.5f - __builtin_fabsf(tf - r);
             const float err = __builtin_fmaf(__builtin_fabsf(hf), e.g_rel, e.g_abs) + __builtin_fabsf(tf) * 0x1p-22f;
-            slow[k] = !((room > err) & (err < 0.25f) & (__builtin_fabsf(hf) < 0x1p64f) &
-                        (vi < (1 << 24)) & (vi > -(1 << 24)));
+            m = 0;
+            return !((room > err) & (err < 0.25f) & (__builtin_fabsf(hf) < 0x1p64f) & (vi < (1 << 24)) &
+                     (vi > -(1 << 24)));
           }
-          any_slow |= slow[k];
+        };
+        bool slow[4], any_slow = false;
+        uint32_t worst = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float r;
+          uint32_t m;
+          slow[k] = decide(k, r, m);
+          if constexpr (F32X) worst = __builtin_elementwise_max(worst, m);
+          else any_slow |= slow[k];
           packed = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, lo128, hi128), k, packed);
         }
+        if constexpr (F32X) any_slow = worst >= __float_as_uint(e.g_lim);
         packed ^= 0x80808080u;
         if (__builtin_expect(__any(any_slow), 0)) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float r;
+            uint32_t m;
+            if constexpr (F32X) slow[k] = decide(k, r, m);
+          }
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (slow[k]) {
@@ -575,9 +594,8 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
       img = gm / e.tokens;
       t = gm - img * e.tokens;
     }
-    auto row_step = [&](int it, float4 r4) {
-      const int rl = it * 4 + (lane >> 4);
-      const v4i a4 = *reinterpret_cast<const v4i*>(stg + rl * 72 + c4);
+    auto row_acc = [&](int it) { return *reinterpret_cast<const v4i*>(stg + (it * 4 + (lane >> 4)) * 72 + c4); };
+    auto row_step = [&](v4i a4, float4 r4) {
       if (gm < M && cok) epi_row4<EPI, I32, F32X>(e, gm, img, t, N, cc, a4, r4);
       gm += 4;
       if constexpr (EPI == EPI_QKV) {
@@ -587,10 +605,16 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
     };
     if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-      for (int it = 0; it < RP / 4; ++it) row_step(it, rv[it]);
+      for (int it = 0; it < RP / 4; ++it) row_step(row_acc(it), rv[it]);
     } else {
+      // the next row's accumulators are read from LDS while this row is computed
+      v4i nxt = row_acc(0);
 #pragma unroll 2
-      for (int it = 0; it < RP / 4; ++it) row_step(it, make_float4(0, 0, 0, 0));
+      for (int it = 0; it < RP / 4; ++it) {
+        const v4i cur = nxt;
+        if (it + 1 < RP / 4) nxt = row_acc(it + 1);
+        row_step(cur, make_float4(0, 0, 0, 0));
+      }
     }
     wave_lds_sync();
   }

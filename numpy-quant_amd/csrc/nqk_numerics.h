@@ -110,7 +110,7 @@ __device__ __forceinline__ float gelu_ref(float h, double rdiv, float add1, floa
 constexpr float GELU_REL = 0x1p-20f, GELU_ABS = 0x1p-60f;
 // With A&S 7.1.26 erf(x) = 1 - P(t) t e^{-x^2}, t = 1 / (1 + p|x|), x = h / sqrt2, the
 // GELU h (1 + erf(x)) / 2 is max(h, 0) - |h| q with q = P(t) t e^{-h^2/2} / 2 (the 1/2
-// and 1/sqrt2 folded into the constants): 12 VALU + v_rcp + v_exp.
+// and 1/sqrt2 folded into the constants): 11 VALU + v_rcp + v_exp.
 __device__ __forceinline__ float gelu_fast(float h) {
   const float ah = __builtin_fabsf(h);
   const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f * 0.70710677f, ah, 1.0f));
@@ -120,7 +120,7 @@ __device__ __forceinline__ float gelu_fast(float h) {
   p = __builtin_fmaf(p, t, 0.5f * 0.254829592f);
   const float e = __builtin_amdgcn_exp2f(h * (h * -0.72134752f));  // e^{-h^2/2}
   const float q = (p * t) * e;
-  return __builtin_fmaxf(h, 0.0f) - ah * q;
+  return __builtin_fmaf(-ah, q, __builtin_fmaxf(h, 0.0f));  // one rounding for max(h, 0) - |h| q
 }
 
 // ------------------------------------------------------------------ NumPy pairwise sum

@@ -14,6 +14,11 @@ for lib in default ${LIBS:-}; do
   NQK_PROJ_GELU=1 GM_LIB=$L GM_ONLY=up:fused timeout -k 10 120 python -u tools/gemm_micro.py >> $o 2>&1 || exit 1
   GM_LIB=$L GM_ONLY=up:fused timeout -k 10 120 python -u tools/gemm_micro.py >> $o 2>&1 || exit 1
 done
+for lib in default ${ATTN_LIBS:-}; do
+  if [ $lib = default ]; then L=""; else L=tools/diag/libnqk_$lib.so; fi
+  echo "== attention $lib" >> $o
+  GM_LIB=$L timeout -k 10 120 python -u tools/attn_micro.py >> $o 2>&1 || exit 1
+done
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench3.json 2> gpurun_out/bench3.err || exit 1
 NQK_PROJ_GELU=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench3g.json 2> gpurun_out/bench3g.err || exit 1
 python - >> $o <<'PY'
