@@ -8,12 +8,14 @@ Workloads (--config):
             are not in the repo), int8, batch 256 per GPU (BASELINE.json configs[2];
             N GPUs = configs[3], independent replicas).
   vit_int4  the same at bit width 4 with nibble-packed weights (configs[4]).
+  vit_tiny  the metric's "ViT-tiny": the same graph re-dimensioned to ViT-Ti/16 (width 192,
+            3 heads of 64, MLP 768, 12 layers; onnx_proto.redimension), int8, batch 256.
   mlp4096   mlp.onnx int8, batch 4096 (configs[1]), replayed as one hipGraph.
 A "step" is one full quantized forward of one synthetic batch already resident in HBM
 (input quantize ... classifier Gemm requantize + output dequantize), through the
 public call path: QModel.__call__ compiles the fused device plan on first use.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config vit|vit_int4|mlp4096]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config vit|vit_int4|vit_tiny|mlp4096]
 
 Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) each process is one
 rank and WORLD_SIZE must equal --gpus.  Without it, `--gpus N` (N > 1) spawns the N
@@ -97,7 +99,7 @@ def spawn_ranks(n: int, argv: list[str], timeout: float | None = None) -> int:
 
 
 # ----------------------------------------------------------------------------- models
-def build_vit(batch: int, bit_width: int, group, calib_batch: int = 8):
+def build_vit(batch: int, bit_width: int, group, calib_batch: int = 8, tiny: bool = False):
     """Model.from_onnx + calibration on rank 0 (8 images) + the graph rewrite of
     Model.quantize; rank 0's QModel reaches every other rank as one RCCL broadcast of
     its packed blob.  Returns (model, qmodel), rebatched to `batch`."""
@@ -105,6 +107,8 @@ def build_vit(batch: int, bit_width: int, group, calib_batch: int = 8):
     from numpy_quant import onnx_proto
     from numpy_quant.model import Model
     proto = onnx_proto.load(MODEL_FILE, synthetic_weights=True)
+    if tiny:  # ViT-Ti/16: the same graph re-dimensioned (width 192, 3 heads, MLP 768)
+        onnx_proto.redimension(proto, *VIT_TINY)
     model = Model.from_onnx(proto)
     qmodel = None
     if group.rank == 0:
@@ -122,6 +126,7 @@ def build_vit(batch: int, bit_width: int, group, calib_batch: int = 8):
     return model, qmodel
 
 
+VIT_TINY = (192, 3, 768)  # ViT-Ti/16: width, heads, MLP width (head size 64 and depth 12 as ViT-Base)
 PROJ_TAGS = ("qgemm_qkv", "qgemm_resid", "qgemm_gelu")  # MatMuls with constant weights (k_proj / k_qgemm_big)
 
 
@@ -199,16 +204,19 @@ def host_cpu() -> dict:
     return {"cpu_model": model, "nproc": os.cpu_count()}
 
 
-def cpu_baseline_vit(bit_width: int) -> dict:
+def cpu_baseline_vit(bit_width: int, tiny: bool = False) -> dict:
     """The oracle (CPU restatement of the reference, int64 np.matmul) on a bounded
     sample: one ViT-Base encoder layer at batch 1 (12 of these are 99 % of a
     forward), scaled x12 to a per-image rate."""
     import numpy as np
     from numpy_quant import onnx_proto
     from oracle import nq_oracle as O
-    g = O.Graph(onnx_proto.load(LAYER_FILE, synthetic_weights=True))
+    proto = onnx_proto.load(LAYER_FILE, synthetic_weights=True)
+    if tiny:
+        onnx_proto.redimension(proto, *VIT_TINY)
+    g = O.Graph(proto)
     rng = np.random.default_rng(7)
-    x = rng.standard_normal((1, 197, 768)).astype(np.float32)
+    x = rng.standard_normal((1, 197, VIT_TINY[0] if tiny else 768)).astype(np.float32)
     with np.errstate(all="ignore"):
         qp, qc = O.calibrate(g, [x], bit_width)
         t0 = time.perf_counter()
@@ -216,7 +224,7 @@ def cpu_baseline_vit(bit_width: int) -> dict:
         dt = time.perf_counter() - t0
     per_image = 12 * dt
     res = {"value": 1.0 / per_image, "unit": "samples/s", "cores": 1, "kind": "port",
-           "sample": f"oracle QModel forward of 1 ViT-Base encoder layer, batch 1 ({dt:.1f} s), x12 layers; "
+           "sample": f"oracle QModel forward of 1 ViT-{'Ti' if tiny else 'Base'} encoder layer, batch 1 ({dt:.1f} s), x12 layers; "
                      "int64 np.matmul is single-threaded (99% of the time)"}
     res.update(host_cpu())
     return res
@@ -270,8 +278,9 @@ def run_vit(args, group):
     from numpy_quant.tensor import FTensor
     rank, world = group.rank, group.world
     bw = 4 if args.config == "vit_int4" else args.bit_width
+    tiny = args.config == "vit_tiny"
     t_setup = time.time()
-    model, qmodel = build_vit(args.batch, bw, group)
+    model, qmodel = build_vit(args.batch, bw, group, tiny=tiny)
     log(f"[bench] model built + calibrated in {time.time() - t_setup:.1f}s")
 
     rng = np.random.default_rng(256 + rank)
@@ -305,9 +314,11 @@ def run_vit(args, group):
         return None
     achieved = proj["ops"] / (proj["ms"] * 1e-3) / 1e12
     res = result_head(args, world, ms_per_step, value, f"int{bw}")
-    res["config"] = {"workload": f"vit_image_classifier (reference models/vit graph = ViT-Base/16-224), "
+    arch = ("ViT-Ti/16-224: the graph re-dimensioned to width 192, 3 heads, MLP 768 (onnx_proto.redimension)"
+            if tiny else "ViT-Base/16-224")
+    res["config"] = {"workload": f"vit_image_classifier (reference models/vit graph, {arch}), "
                                  f"QModel.__call__ (fused plan), int{bw}, batch {args.batch}/GPU",
-                     "model": "vit_image_classifier_no_weights.onnx (ViT-Base/16-224)",
+                     "model": f"vit_image_classifier_no_weights.onnx ({arch})",
                      "global_batch": args.batch * world, "seq_len": 197,
                      "parallelism": f"replicas x{world}",
                      "executor": "fused plan" + (", hipGraph replay" if graph else "") +
@@ -324,7 +335,7 @@ def run_vit(args, group):
     res["kernels"] = kern
     res.update(ver)
     if not args.no_cpu_baseline and world == 1:
-        res["cpu_baseline"] = cpu_baseline_vit(bw)
+        res["cpu_baseline"] = cpu_baseline_vit(bw, tiny)
     return res
 
 
@@ -400,7 +411,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--bit-width", type=int, default=8)
-    ap.add_argument("--config", choices=("vit", "vit_int4", "mlp4096"), default="vit")
+    ap.add_argument("--config", choices=("vit", "vit_int4", "vit_tiny", "mlp4096"), default="vit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=0, help="1: replay the ViT forward as one captured hipGraph")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # launcher test: no GPU

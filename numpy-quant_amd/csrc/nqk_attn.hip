@@ -15,7 +15,7 @@
 //   Ks   [NT*32][64]     int8, 16-byte chunks XOR-swizzled (conflict-free A reads)
 //   Vt   [64][PST]       int8 V^T, zero padded to NT*32 tokens; PST = NT*32 + 16
 //   colK [NT*32], colV [64]   int32 zero-point column terms
-// 30 KiB per workgroup: two workgroups (8 waves) per CU; everything else is in VGPRs.
+// 30 KiB per workgroup: three workgroups (12 waves) per CU; everything else is in VGPRs.
 #include "nqk_common.h"
 #include "nqk_numerics.h"
 
@@ -96,8 +96,21 @@ __device__ __forceinline__ float xor32f(float x) { return __int_as_float(xor32i(
 // 2^24, host-checked), the scores Div is a power of two (an exact f32 multiply), and the
 // P / context quantizations go through a rounding filter (t from one f32 product, exact
 // chain for any element within the product's error bound of a rounding boundary).
+#ifndef NQK_ATTN_WPE
+#define NQK_ATTN_WPE 0  // diagnostic builds: amdgpu_waves_per_eu(NQK_ATTN_WPE) occupancy target
+#endif
+#if NQK_ATTN_WPE
+#define NQK_ATTN_OCC __attribute__((amdgpu_waves_per_eu(NQK_ATTN_WPE, NQK_ATTN_WPE)))
+#else
+#define NQK_ATTN_OCC
+#endif
+// three workgroups (12 waves) per CU: the register budget is 168 per lane (the exp /
+// quantize phases are VALU-issue-bound, so the third wave per SIMD pays for a few spills)
+#ifndef NQK_ATTN_MINB
+#define NQK_ATTN_MINB 3
+#endif
 template <int NT, int TC, bool FAST>  // TC: compile-time token count (0: runtime a.T)
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, NQK_ATTN_MINB) NQK_ATTN_OCC
 k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int8_t* __restrict__ Vg,
             int8_t* __restrict__ ctx, AttnArgs a) {
   constexpr int TP = NT * 32;  // padded tokens (score columns / PV contraction)
@@ -177,9 +190,20 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     float mx = -__builtin_inff();
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
+      // the accumulators start at -(row term + column term): the MFMAs then leave the
+      // zero-point-corrected integer v = acc - terms itself (int32, exact in any order)
       v16i acc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0;
+      for (int qq = 0; qq < 4; ++qq) {
+        if (pad_group(c, qq)) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[4 * qq + j] = 0;
+          continue;
+        }
+        const v4i ck = *reinterpret_cast<const v4i*>(colK + c * 32 + 8 * qq + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[4 * qq + j] = -(rowterm + ck[j]);
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const v4i ka = *reinterpret_cast<const v4i*>(Ks + swz64a(c * 32 + r32, 2 * s + h));
@@ -192,11 +216,10 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           for (int j = 0; j < 4; ++j) e[c][4 * qq + j] = 0.0f;
           continue;
         }
-        const v4i ck = *reinterpret_cast<const v4i*>(colK + c * 32 + 8 * qq + 4 * h);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * qq + j, n = c * 32 + 8 * qq + 4 * h + j;
-          const int vv = acc[r] - rowterm - ck[j];
+          const int vv = acc[r];
           float y;
           // FAST: RN(v s) / 2^k == RN(v (s / 2^k)) while both are normal (host-checked)
           if constexpr (FAST) y = (float)vv * a.s_qkd;
@@ -289,7 +312,10 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         // element: the product, rint, the distance test, then v + 128 (v = the clamped
         // integer, in [0, 255]) converted straight into its byte (v_cvt_pk_u8_f32) and
         // the bytes flipped to two's complement at once (^ 0x80 each).
-        uint32_t slow = 0;
+        // the tile's largest distance |tf - r| (tf finite: e in [0, 1], kpf finite),
+        // one v_max per element; a tile with any element at or past plim recomputes the
+        // same tf per element and sends those elements through the exact chain
+        float worst = 0.0f;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           if (pad_group(c, qq)) {
@@ -302,21 +328,22 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             const int n = c * 32 + 8 * qq + 4 * h + j;
             const float tf = e[c][4 * qq + j] * kpf;
             const float r = __builtin_rintf(tf);
-            slow |= (uint32_t)!(__builtin_fabsf(tf - r) < plim) << (4 * qq + j);
+            worst = __builtin_fmaxf(worst, __builtin_fabsf(tf - r));
             float v = __builtin_amdgcn_fmed3f(r + zp128, lo128, hi128);
             v = n < T ? v : 128.0f;  // padded columns: 0
             packed = __builtin_amdgcn_cvt_pk_u8_f32(v, j, packed);
           }
           dw[qq] = (int)(packed ^ 0x80808080u);
         }
-        if (__builtin_expect(__any(slow != 0), 0)) {
+        if (__builtin_expect(__any(!(worst < plim)), 0)) {
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq) {
             if (pad_group(c, qq)) continue;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int n = c * 32 + 8 * qq + 4 * h + j;
-              if ((slow >> (4 * qq + j)) & 1) {
+              const float tf = e[c][4 * qq + j] * kpf;
+              if (!(__builtin_fabsf(tf - __builtin_rintf(tf)) < plim)) {
                 const int qv = n < T ? quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) : 0;
                 dw[qq] = (int)(((uint32_t)dw[qq] & ~(0xffu << (8 * j))) | ((uint32_t)(qv & 0xff) << (8 * j)));
               }

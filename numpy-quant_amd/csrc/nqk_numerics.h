@@ -62,9 +62,9 @@ __device__ __forceinline__ float np_expf(float x) { return np_expf_t<true>(x); }
 // (nqk_selftest_fastmath, counts[2]).
 __device__ __forceinline__ float np_expf_nonpos(float x) {
   const bool under = x <= -103.97208404541015625f;
-  float q = x * 1.442695040888963407359924681001892137f;
-  q = q + 0x1.800000p+23f;
-  q = q - 0x1.800000p+23f;
+  // rint by v_rndne_f32: the same integer as NumPy's magic-number add / subtract for
+  // |x log2 e| < 2^22, and every larger |q| belongs to an x the final select zeroes
+  const float q = __builtin_rintf(x * 1.442695040888963407359924681001892137f);
   float r = __builtin_fmaf(q, -6.93145752e-1f, x);
   r = __builtin_fmaf(q, -1.42860677e-6f, r);
   float num = __builtin_fmaf(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);

@@ -427,3 +427,44 @@ def rebatch(m: ModelProto, batch: int) -> int:
         if vi.shape and vi.shape[0] == 1:
             vi.shape[0] = batch
     return count
+
+
+def redimension(m: ModelProto, width: int, heads: int, mlp: int, seed: int = 0,
+                base: tuple[int, int, int] = (768, 12, 3072)) -> int:
+    """Re-dimension a ViT graph exported at base = (width, heads, mlp) (the reference's
+    ViT-Base/16 graphs, models/vit.py:43) to another ViT family member with the same head
+    size and depth, e.g. ViT-Ti/16 = (192, 3, 768): every initializer dimension equal to
+    the base width / MLP width is rewritten and its weights re-synthesized
+    (`synthetic_array`, same names and seed), and the Reshape shape constants
+    [b, t, heads, head_dim] / [b, t, width] follow.  Only for graphs whose weights are
+    synthetic (the reference ships none).  Returns the number of tensors rewritten."""
+    w0, h0, f0 = base
+    if w0 // h0 != width // heads or width % heads:
+        raise ValueError("redimension keeps the head size: width / heads must equal the base's")
+    dmap = {w0: width, f0: mlp}
+    count = 0
+    for t in m.graph.initializer:
+        dims = [dmap.get(int(d), int(d)) for d in t.dims]
+        if dims != [int(d) for d in t.dims]:
+            t.set_array(synthetic_array(t.name, tuple(dims), seed))
+            count += 1
+    for node in m.graph.node:
+        if node.op_type != "Constant":
+            continue
+        for a in node.attribute:
+            if a.name != "value" or a.t is None:
+                continue
+            v = a.t.to_array()
+            if v.dtype != np.int64 or v.ndim != 1:
+                continue
+            if v.shape[0] == 4 and v[2] == h0 and v[3] == w0 // h0:
+                v = v.copy()
+                v[2] = heads
+            elif v.shape[0] == 3 and v[2] == w0:
+                v = v.copy()
+                v[2] = width
+            else:
+                continue
+            a.t.set_array(v)
+            count += 1
+    return count

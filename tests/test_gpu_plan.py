@@ -148,3 +148,37 @@ def test_plan_restores_stream_after_error():
     _lib.call("nqk_set_stream", 0)
     _lib.call("nqk_stream", ctypes.byref(base))
     assert cur.value == base.value
+
+
+def test_vit_tiny_fused_plan_matches_node_loop_and_oracle():
+    """The metric's ViT-tiny (the reference's ViT graph re-dimensioned to ViT-Ti/16 by
+    onnx_proto.redimension: width 192, 3 heads of 64, MLP 768): the fused plan at batch 3
+    equals the node-by-node loop image by image, and batch 1 equals the oracle's
+    restatement of the reference (quantized forward with the oracle's calibration) bit
+    for bit."""
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model, QuantizationParams
+    from oracle import nq_oracle as O
+    path = os.path.join(MODELS, "vit_image_classifier_no_weights.onnx")
+    rng = np.random.default_rng(21)
+    x = rng.standard_normal((3, 3, 224, 224)).astype(np.float32)
+    proto = onnx_proto.load(path, synthetic_weights=True)
+    assert onnx_proto.redimension(proto, 192, 3, 768) > 0
+    graph = O.Graph(proto)
+    with np.errstate(all="ignore"):
+        qp, qc = O.calibrate(graph, [x[:1]], 8)
+        ref = O.outputs_of(graph, O.quantized_forward(graph, qp, qc, [x[:1]], 8))[0]
+    model = Model.from_onnx(proto)
+    # the oracle's parameters (its calibration runs the box's own OpenBLAS, whose kernel
+    # family may differ from the fixtures' host; device calibration is pinned there)
+    qmodel = model.quantize_with({k: QuantizationParams(v.scale, v.zero_point) for k, v in qp.items()}, bit_width=8)
+    qmodel.keep_values = True
+    np.testing.assert_array_equal(qmodel([x[:1]])[0], ref)
+    model.rebatch(3)
+    eager = qmodel([x])[0]
+    qmodel.keep_values = False
+    plan = qmodel.compile()
+    assert plan.fused == 12
+    out = qmodel([x])[0]
+    np.testing.assert_array_equal(out, eager)
+    np.testing.assert_array_equal(out[:1], ref)
