@@ -62,10 +62,10 @@ int nqk_memcpy_d2d(void* dst, const void* src, size_t bytes);   /* async */
 int nqk_memset(void* ptr, int value, size_t bytes);             /* async */
 int nqk_sync(void);
 int nqk_stream(void** stream);         /* the library's hipStream_t */
-/* a second stream for independent work (the fused plan's two half batches):
- * nqk_set_stream(1) routes every later call to it, nqk_set_stream(0) back;
- * nqk_stream_fork makes stream 1 wait for all work issued so far on stream 0,
- * nqk_stream_join makes stream 0 wait for all work issued so far on stream 1. */
+/* side streams 1..3 for independent work (the fused plan's batch parts):
+ * nqk_set_stream(s) routes every later call to stream s, nqk_set_stream(0) back;
+ * nqk_stream_fork makes every side stream wait for all work issued so far on stream 0,
+ * nqk_stream_join makes stream 0 wait for all work issued so far on the side streams. */
 int nqk_set_stream(int which);
 int nqk_stream_fork(void);
 int nqk_stream_join(void);

@@ -235,7 +235,7 @@ struct EmbedEpi {
   int64_t hw;
 };
 
-template <bool EMBED, bool AL16>
+template <bool EMBED, bool AL16, bool VEC = false>
 __global__ void __launch_bounds__(256, 2)
 k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
              int64_t N, int64_t K, int64_t a_sm, int64_t a_sk, int64_t b_sk, int64_t b_sn, int64_t ldc,
@@ -250,7 +250,23 @@ k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __
   const int wm = wave >> 1, wn = wave & 1, r32 = lane & 31, h = lane >> 5;
   const int64_t m0 = (int64_t)blockIdx.y * 128, n0 = (int64_t)blockIdx.x * 128;
   float ra[8], rb[8];
+  // VEC (unit k stride of A, unit n stride of B, K % 16 == 0, N % 4 == 0, 16-byte
+  // aligned rows): the same tiles by two 16-byte loads per operand and thread
+  float4 va[2], vb[2];
   auto load = [&](int64_t k0) {
+    if constexpr (VEC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + i * 256;
+        const int r = idx >> 2, c = idx & 3;      // A: row r, k 4c .. 4c + 3
+        const int64_t gm = m0 + r;
+        va[i] = gm < M ? *reinterpret_cast<const float4*>(A + gm * a_sm + k0 + 4 * c) : make_float4(0, 0, 0, 0);
+        const int kr = idx >> 5, cc = (idx & 31) * 4;  // B: k row kr, columns cc .. cc + 3
+        const int64_t bn = n0 + cc;
+        vb[i] = bn < N ? *reinterpret_cast<const float4*>(B + (k0 + kr) * b_sk + bn) : make_float4(0, 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int idx = tid + i * 256;
@@ -263,6 +279,19 @@ k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __
     }
   };
   auto store = [&](int buf) {
+    if constexpr (VEC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + i * 256;
+        const int r = idx >> 2, c = idx & 3;
+        sa[buf][4 * c + 0][r] = va[i].x;
+        sa[buf][4 * c + 1][r] = va[i].y;
+        sa[buf][4 * c + 2][r] = va[i].z;
+        sa[buf][4 * c + 3][r] = va[i].w;
+        *reinterpret_cast<float4*>(&sb[buf][idx >> 5][(idx & 31) * 4]) = vb[i];
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int idx = tid + i * 256;
@@ -606,7 +635,13 @@ extern "C" int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch
   if ((K & 1) == 0 && K > 0 && M * N >= 128 * 128 && !getenv("NQK_SGEMM_VALU")) {
     dim3 g2((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128), (unsigned)batch);
     if ((M + 127) / 128 > 65535) return fail("nqk_sgemm: grid too large");
-    if (kblocks_al16(K, kb))
+    const bool vec = a_sk == 1 && b_sn == 1 && (N % 4) == 0 && (a_sm % 4) == 0 && (b_sk % 4) == 0 &&
+                     (a_mat_stride % 4) == 0 && (b_mat_stride % 4) == 0 &&
+                     ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0 && !getenv("NQK_SGEMM_SCALAR");
+    if (kblocks_al16(K, kb) && vec)
+      hipLaunchKernelGGL((k_sgemm_mfma<false, true, true>), g2, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk,
+                         b_sk, b_sn, ldc, m, a_mat_stride, b_mat_stride, c_mat_stride, kb, EmbedEpi{nullptr, nullptr, 1});
+    else if (kblocks_al16(K, kb))
       hipLaunchKernelGGL((k_sgemm_mfma<false, true>), g2, dim3(256), 0, stream(), a, b, c, M, N, K, a_sm, a_sk, b_sk,
                          b_sn, ldc, m, a_mat_stride, b_mat_stride, c_mat_stride, kb, EmbedEpi{nullptr, nullptr, 1});
     else
@@ -630,7 +665,11 @@ extern "C" int nqk_sgemm_embed(const float* cols, const float* w, const float* b
   if (blas_kblocks(K, &kb)) return fail("nqk_sgemm_embed: K too large for the BLAS blocking table");
   const BatchMap m = batch_map(nullptr);
   dim3 g2((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128), 1);
-  if (kblocks_al16(K, kb))
+  const bool vec = (N % 4) == 0 && ((((uintptr_t)cols) | ((uintptr_t)w)) & 15) == 0 && !getenv("NQK_SGEMM_SCALAR");
+  if (kblocks_al16(K, kb) && vec)
+    hipLaunchKernelGGL((k_sgemm_mfma<true, true, true>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1,
+                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
+  else if (kblocks_al16(K, kb))
     hipLaunchKernelGGL((k_sgemm_mfma<true, true>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1, N,
                        (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
   else

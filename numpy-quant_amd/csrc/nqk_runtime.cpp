@@ -9,9 +9,10 @@ namespace {
 thread_local std::string g_err;
 int g_device = -1;
 hipStream_t g_streams[64] = {};
-hipStream_t g_side[64] = {};   // the second stream (nqk_set_stream(1))
-int g_cur = 0;                 // current stream index of the (single) host thread
-hipEvent_t g_fork = nullptr, g_join = nullptr;
+constexpr int kSide = 3;           // side streams 1..3 (nqk_set_stream)
+hipStream_t g_side[64][kSide] = {};
+int g_cur = 0;                     // current stream index of the (single) host thread
+hipEvent_t g_fork = nullptr, g_join[kSide] = {};
 hipEvent_t g_t0 = nullptr, g_t1 = nullptr;
 hipGraph_t g_capturing = nullptr;
 std::mutex g_mu;
@@ -25,7 +26,7 @@ int check(hipError_t e, const char* what) {
 }
 hipStream_t stream() {
   if (g_device < 0) nqk_init(0);
-  return g_cur ? g_side[g_device] : g_streams[g_device];
+  return g_cur ? g_side[g_device][g_cur - 1] : g_streams[g_device];
 }
 }  // namespace nqk
 
@@ -76,25 +77,26 @@ int nqk_memset(void* ptr, int value, size_t bytes) {
   return check(hipMemsetAsync(ptr, value, bytes, stream()), "memset");
 }
 int nqk_sync(void) {
-  if (g_device >= 0 && g_side[g_device] && check(hipStreamSynchronize(g_side[g_device]), "hipStreamSynchronize"))
-    return -1;
+  for (int i = 0; g_device >= 0 && i < kSide; ++i)
+    if (g_side[g_device][i] && check(hipStreamSynchronize(g_side[g_device][i]), "hipStreamSynchronize")) return -1;
   return check(hipStreamSynchronize(g_device >= 0 ? g_streams[g_device] : stream()), "hipStreamSynchronize");
 }
 
 static int ensure_side() {
   if (g_device < 0 && nqk_init(0)) return -1;
-  if (!g_side[g_device] &&
-      check(hipStreamCreateWithFlags(&g_side[g_device], hipStreamNonBlocking), "hipStreamCreate"))
-    return -1;
-  if (!g_fork && (check(hipEventCreateWithFlags(&g_fork, hipEventDisableTiming), "hipEventCreate") ||
-                  check(hipEventCreateWithFlags(&g_join, hipEventDisableTiming), "hipEventCreate")))
-    return -1;
+  for (int i = 0; i < kSide; ++i) {
+    if (!g_side[g_device][i] &&
+        check(hipStreamCreateWithFlags(&g_side[g_device][i], hipStreamNonBlocking), "hipStreamCreate"))
+      return -1;
+    if (!g_join[i] && check(hipEventCreateWithFlags(&g_join[i], hipEventDisableTiming), "hipEventCreate")) return -1;
+  }
+  if (!g_fork && check(hipEventCreateWithFlags(&g_fork, hipEventDisableTiming), "hipEventCreate")) return -1;
   return 0;
 }
 
 int nqk_set_stream(int which) {
-  if (which != 0 && which != 1) return fail("nqk_set_stream: 0 or 1");
-  if (which == 1 && ensure_side()) return -1;
+  if (which < 0 || which > kSide) return fail("nqk_set_stream: 0 .. 3");
+  if (which && ensure_side()) return -1;
   g_cur = which;
   return 0;
 }
@@ -102,13 +104,18 @@ int nqk_set_stream(int which) {
 int nqk_stream_fork(void) {
   if (ensure_side()) return -1;
   if (check(hipEventRecord(g_fork, g_streams[g_device]), "hipEventRecord")) return -1;
-  return check(hipStreamWaitEvent(g_side[g_device], g_fork, 0), "hipStreamWaitEvent");
+  for (int i = 0; i < kSide; ++i)
+    if (check(hipStreamWaitEvent(g_side[g_device][i], g_fork, 0), "hipStreamWaitEvent")) return -1;
+  return 0;
 }
 
 int nqk_stream_join(void) {
   if (ensure_side()) return -1;
-  if (check(hipEventRecord(g_join, g_side[g_device]), "hipEventRecord")) return -1;
-  return check(hipStreamWaitEvent(g_streams[g_device], g_join, 0), "hipStreamWaitEvent");
+  for (int i = 0; i < kSide; ++i) {
+    if (check(hipEventRecord(g_join[i], g_side[g_device][i]), "hipEventRecord")) return -1;
+    if (check(hipStreamWaitEvent(g_streams[g_device], g_join[i], 0), "hipStreamWaitEvent")) return -1;
+  }
+  return 0;
 }
 int nqk_stream(void** s) { *s = (void*)stream(); return 0; }
 
@@ -139,13 +146,14 @@ int nqk_graph_begin(void) {
   return check(hipStreamBeginCapture(stream(), hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
 }
 int nqk_graph_abort(void) {
-  // a capture that failed part-way: join the side stream back (it may be part of the
+  // a capture that failed part-way: join the side streams back (they may be part of the
   // capture after a fork), end the capture and drop the partial graph
   g_cur = 0;
-  if (g_device >= 0 && g_side[g_device] && g_join) {
-    (void)hipEventRecord(g_join, g_side[g_device]);
-    (void)hipStreamWaitEvent(g_streams[g_device], g_join, 0);
-  }
+  for (int i = 0; g_device >= 0 && i < kSide; ++i)
+    if (g_side[g_device][i] && g_join[i]) {
+      (void)hipEventRecord(g_join[i], g_side[g_device][i]);
+      (void)hipStreamWaitEvent(g_streams[g_device], g_join[i], 0);
+    }
   hipGraph_t g = nullptr;
   (void)hipStreamEndCapture(stream(), &g);
   if (g) (void)hipGraphDestroy(g);

@@ -42,17 +42,19 @@ Epilogue = _lib.Epilogue
 
 
 class Streams:
-    """Fork / join bookkeeping of Plan.run's two HIP streams.
+    """Fork / join bookkeeping of Plan.run's HIP streams.
 
-    A split step runs its images in two halves, half 0 on stream 0 and half 1 on
-    stream 1 (nqk_set_stream); consecutive split steps use the same halves, so each
-    stream only depends on its own earlier work and no event is needed between them.
-    Whole-batch work (eager nodes, a dequantized layer input, an unsplit layer) must
-    first `join()` (stream 0 waits for stream 1); halves that follow whole-batch work
-    on stream 0 must first `fork()` (stream 1 waits for stream 0)."""
+    A split step runs its images in `parts` consecutive parts (2 by default,
+    NQK_STREAMS = 2..4), part i on stream i (nqk_set_stream); consecutive split steps
+    use the same parts, so each stream only depends on its own earlier work and no
+    event is needed between them.  Whole-batch work (eager nodes, a dequantized layer
+    input, an unsplit layer) must first `join()` (stream 0 waits for the side streams);
+    parts that follow whole-batch work on stream 0 must first `fork()` (the side
+    streams wait for stream 0)."""
 
-    def __init__(self, enabled: bool):
+    def __init__(self, enabled: bool, parts: int = 2):
         self.enabled = enabled
+        self.parts = max(1, min(4, int(parts)))
         self.forked = False
 
     def fork(self):
@@ -66,19 +68,22 @@ class Streams:
             self.forked = False
 
     def halves(self, n: int, fn):
-        """fn(stream_index, first_image, images) for the two halves of n images on the
-        two streams (or once, whole batch on stream 0, when splitting is off / n < 2);
-        the current stream is back to 0 afterwards, also when fn raises."""
-        if not self.enabled or n < 2:
+        """fn(stream_index, first_image, images) for the parts of n images on their
+        streams (or once, whole batch on stream 0, when splitting is off / n < 2); the
+        current stream is back to 0 afterwards, also when fn raises."""
+        p = min(self.parts, n)
+        if not self.enabled or p < 2:
             self.join()
             fn(0, 0, n)
             return
         self.fork()
-        h = n // 2
         try:
-            for s_idx, (i0, nb) in enumerate(((0, h), (h, n - h))):
+            i0 = 0
+            for s_idx in range(p):
+                nb = n // p + (1 if s_idx < n % p else 0)
                 _lib.call("nqk_set_stream", s_idx)
                 fn(s_idx, i0, nb)
+                i0 += nb
         finally:
             _lib.call("nqk_set_stream", 0)
 
@@ -848,7 +853,7 @@ class Plan:
                 self.fused += 1
 
     def run(self, qmodel, times=None, profile=False):
-        streams = Streams(self.split)
+        streams = Streams(self.split, int(os.environ.get("NQK_STREAMS", "2")))
         try:
             for kind, obj in self.steps:
                 if kind == "node":

@@ -214,3 +214,28 @@ def test_one_row_gemm_takes_gemv_order():
     x1 = rng.standard_normal((1, 768)).astype(np.float32)
     y1 = onnx_operator_implementation("Gemm", [FTensor(x1), FTensor(w), FTensor(b)], {"transB": 1})[0].data
     np.testing.assert_array_equal(y1, (sgemv_t(w, x1[0], 8) + b)[None, :])
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 768, 768), (197, 192, 768), (130, 260, 64), (50176 // 16, 768, 768)])
+def test_sgemm_vector_loads_equal_scalar_loads(M, N, K, monkeypatch):
+    """k_sgemm_mfma's 16-byte operand loads (unit-stride A rows and B rows) give the same
+    bits as its scalar-load form (NQK_SGEMM_SCALAR=1), plain and patch-embedding paths."""
+    from numpy_quant import kernels as KM
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    rng = np.random.default_rng(M + N + K)
+    a = DeviceArray.from_host(rng.standard_normal((M, K), dtype=np.float32))
+    b = DeviceArray.from_host(rng.standard_normal((K, N), dtype=np.float32))
+    got = KM.sgemm(a, K, 1, b, N, 1, M, N, K).to_host()
+    hw = M  # one image of M patches through the embedding epilogue
+    bias = DeviceArray.from_host(rng.standard_normal(N, dtype=np.float32))
+    cls = DeviceArray.from_host(rng.standard_normal(N, dtype=np.float32))
+    pos = DeviceArray.from_host(rng.standard_normal((hw + 1, N), dtype=np.float32))
+    out = DeviceArray((1, hw + 1, N), np.float32)
+    _lib.call("nqk_sgemm_embed", a.vp, b.vp, bias.vp, cls.vp, pos.vp, out.vp, 1, hw, N, K)
+    emb = out.to_host()
+    monkeypatch.setenv("NQK_SGEMM_SCALAR", "1")
+    ref = KM.sgemm(a, K, 1, b, N, 1, M, N, K).to_host()
+    _lib.call("nqk_sgemm_embed", a.vp, b.vp, bias.vp, cls.vp, pos.vp, out.vp, 1, hw, N, K)
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(emb, out.to_host())
