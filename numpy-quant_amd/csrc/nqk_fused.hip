@@ -568,17 +568,20 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
   const int gn0 = ncol0 + c4;
   const bool cok = gn0 < N;  // N % 4 == 0 (host-checked): the 4 columns are valid together
   EpiCol4 cc = epi_col4<EPI>(e, gn0, cok);
+  // residual rows: pass 0's in flight while its tile is staged, every later pass's
+  // issued right after the previous pass is staged (two register sets; the staged
+  // accumulators of earlier passes are dead by then)
+  float4 rv[2][RP / 4];
+  auto load_res = [&](int pass, float4 (&dst)[RP / 4]) {
+#pragma unroll
+    for (int it = 0; it < RP / 4; ++it) {
+      const int gm = min(mw + pass * RP + it * 4 + (lane >> 4), M - 1);
+      dst[it] = cok ? *reinterpret_cast<const float4*>(e.resid + (int64_t)gm * N + gn0) : make_float4(0, 0, 0, 0);
+    }
+  };
+  if constexpr (EPI == EPI_RESID) load_res(0, rv[0]);
 #pragma unroll
   for (int pass = 0; pass < 128 / RP; ++pass) {
-    // residual rows of this pass in flight while the tile is staged
-    float4 rv[RP / 4];
-    if constexpr (EPI == EPI_RESID) {
-#pragma unroll
-      for (int it = 0; it < RP / 4; ++it) {
-        const int gm = min(mw + pass * RP + it * 4 + (lane >> 4), M - 1);
-        rv[it] = cok ? *reinterpret_cast<const float4*>(e.resid + (int64_t)gm * N + gn0) : make_float4(0, 0, 0, 0);
-      }
-    }
 #pragma unroll
     for (int ii = 0; ii < RP / 32; ++ii)
 #pragma unroll
@@ -587,6 +590,8 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
         for (int r = 0; r < 16; ++r)
           stg[(ii * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 72 + j * 32 + r32] = acc[pass * (RP / 32) + ii][j][r] >> ASH;
     wave_lds_sync();
+    if constexpr (EPI == EPI_RESID)
+      if (pass + 1 < 128 / RP) load_res(pass + 1, rv[(pass + 1) & 1]);
     // image / token of this lane's row, advanced incrementally (4 rows per step)
     int gm = mw + pass * RP + (lane >> 4);
     int img = 0, t = 0;
@@ -605,7 +610,7 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
     };
     if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-      for (int it = 0; it < RP / 4; ++it) row_step(row_acc(it), rv[it]);
+      for (int it = 0; it < RP / 4; ++it) row_step(row_acc(it), rv[pass & 1][it]);
     } else {
       // the next row's accumulators are read from LDS while this row is computed
       v4i nxt = row_acc(0);
@@ -1819,7 +1824,14 @@ static int num_cus() {
 template <int EPI, bool F32X, int NK, bool B4>
 static void launch_proj(const int8_t* a, const int8_t* bp, int64_t M, int64_t N, int64_t lda, const Epi& e) {
   const int tn = (int)(N / GBN), nt = (int)((M + 255) / 256) * tn;
-  const int grid = nt < num_cus() ? nt : num_cus();
+  // workgroups (one per CU): all CUs, or NQK_PROJ_CUS of them (diagnostic: a persistent
+  // GEMM of one stream's half batch leaving CUs to the other stream)
+  static const int cus = [] {
+    const char* v = getenv("NQK_PROJ_CUS");
+    const int n = v ? atoi(v) : 0;
+    return n > 0 && n < num_cus() ? n : num_cus();
+  }();
+  const int grid = nt < cus ? nt : cus;
   const size_t shm = p2_lds(EPI, B4);
   hipLaunchKernelGGL((k_proj<EPI, F32X, NK, B4>), dim3(grid), dim3(512), shm, stream(), a, bp, (int)M, (int)N, (int)lda,
                      tn, nt, e);

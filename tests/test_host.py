@@ -204,3 +204,33 @@ def test_sgemv_order_matches_numpy_matmul(K, N, threads):
     with threadpoolctl.threadpool_limits(limits=threads, user_api="blas"):
         ref = (x[None, :] @ w.T)[0]
     np.testing.assert_array_equal(sgemv_t(w, x, threads).view(np.int32), ref.view(np.int32))
+
+
+def test_redimension_vit_base_to_tiny():
+    """onnx_proto.redimension (the metric's ViT-tiny from the reference's ViT-Base graph):
+    every width-768 / MLP-3072 initializer dimension and the head / width Reshape
+    constants follow (192, 3 heads of 64, 768), the oracle's float forward runs and the
+    synthetic weights stay deterministic."""
+    from oracle import nq_oracle as O
+    path = os.path.join(MODELS, "vit_image_classifier_no_weights.onnx")
+    m = onnx_proto.load(path, synthetic_weights=True)
+    n = onnx_proto.redimension(m, 192, 3, 768)
+    dims = {tuple(t.dims) for t in m.graph.initializer}
+    assert not any(768 in d and d != (192, 768) and d != (768, 192) and d != (768,) for d in dims)
+    assert (192, 3, 16, 16) in dims and (1000, 192) in dims and (192, 768) in dims and (768, 192) in dims
+    consts = [tuple(onnx_proto.to_array(a.t).tolist()) for nd in m.graph.node if nd.op_type == "Constant"
+              for a in nd.attribute if a.name == "value" and onnx_proto.to_array(a.t).dtype == np.int64
+              and onnx_proto.to_array(a.t).ndim == 1 and onnx_proto.to_array(a.t).size in (3, 4)]
+    assert (1, 197, 3, 64) in consts and (1, 197, 192) in consts and (1, 197, 12, 64) not in consts
+    assert n == 247
+    x = np.random.default_rng(0).standard_normal((1, 3, 224, 224)).astype(np.float32)
+    g = O.Graph(m)
+    out = O.outputs_of(g, O.float_forward(g, [x]))[0]
+    assert out.shape == (1, 1000) and np.isfinite(out).all()
+    m2 = onnx_proto.load(path, synthetic_weights=True)
+    onnx_proto.redimension(m2, 192, 3, 768)
+    a = {t.name: onnx_proto.to_array(t) for t in m.graph.initializer}
+    for t in m2.graph.initializer:
+        np.testing.assert_array_equal(onnx_proto.to_array(t), a[t.name])
+    with pytest.raises(ValueError):
+        onnx_proto.redimension(onnx_proto.load(path, synthetic_weights=True), 192, 4, 768)
