@@ -226,6 +226,9 @@ typedef struct nqk_epilogue {
   int32_t b_packed;                     /* 1: bt is an nqk_pack_b image; 2: nqk_pack_b4  */
   const int32_t* colterm;               /* optional: col[n] * zpa as int32 (the persistent */
                                         /* projection GEMM needs it; NULL: not used)     */
+  const int8_t* bt_pg;                  /* optional: the nqk_pack_pg image of the same Bt;  */
+                                        /* when set, the 16x16x64 persistent GEMM (k_pg)  */
+                                        /* runs the cases it takes (NULL: not used)       */
 } nqk_epilogue;
 /* int8 MFMA GEMM C = A . Bt^T (layouts as nqk_qgemm_i8) with a fused epilogue:
  *   QKV    model.py MatMul -> Add(bias) -> Reshape -> Transpose -> quantize, 3 groups
@@ -243,12 +246,21 @@ int nqk_pack_b(const int8_t* bt, int8_t* out, int64_t N, int64_t K, int64_t ldb)
  * ceil(N/256)*256*K/2 bytes; the GEMM unpacks them in registers after the LDS stage
  * (b_packed = 2).  BASELINE configs[4] ("int4 packed weights"). */
 int nqk_pack_b4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t ldb);
+/* Tile-packed copy of Bt [N][K] (K % 64 == 0) for the persistent 16x16x64 projection GEMM
+ * (nqk_epilogue.bt_pg): [ceil(N/256)][K/64] stages of 256 rows x 64 bytes, 16-byte chunks
+ * swizzled for conflict-free fragment reads; each wave's 64 columns permuted so that a lane's
+ * MFMA results are 16 consecutive output columns (layout 0: QKV / GELU, int8 outputs) or
+ * 4 x 4 columns whose 16-byte stores cover 64 contiguous bytes per row (layout 1: the
+ * residual epilogues, f32 outputs); ceil(N/256)*256*K bytes (a layout of the
+ * numpy_quantization.py:44-61 q_matmul operand, replaces no reference function). */
+int nqk_pack_pg(const int8_t* bt, int8_t* out, int64_t N, int64_t K, int64_t ldb, int layout);
 int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, int64_t M, int64_t N, int64_t K,
                     int64_t lda, int64_t ldb, const int64_t* bmap, int64_t a_mat_stride, int64_t b_mat_stride,
                     const nqk_epilogue* params);
 /* Which kernel the last nqk_qgemm_fused call launched (tests / diagnostics): 0 small tiles
  * (k_qgemm_epi), 1 128x256 tiles (k_qgemm_big), 2 ping-pong 256x256 (k_qgemm_pp), 3 the
- * persistent projection GEMM with the epilogue overlapped (k_proj); -1 none yet. */
+ * persistent projection GEMM with the epilogue overlapped (k_proj), 4 the persistent 16x16x64
+ * GEMM with two workgroups per CU (k_pg); -1 none yet. */
 int nqk_qgemm_last_kernel(void);
 /* LayerNormalization (model.py:134-152) fused with the consumer MatMul's quantize */
 int nqk_ln_quant(const float* x, const float* gamma, const float* beta, int8_t* out, int64_t rows, int64_t cols,

@@ -1808,7 +1808,11 @@ static void launch_big(bool pp, const int8_t* a, const int8_t* bt, int64_t M, in
   }
 }
 
-static int g_last_gemm = -1;  // nqk_qgemm_last_kernel: 0 small tiles, 1 big tile, 2 ping-pong, 3 persistent
+static int g_last_gemm = -1;  // nqk_qgemm_last_kernel: 0 small tiles, 1 big tile, 2 ping-pong, 3 persistent, 4 k_pg
+namespace nqk {
+int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, int64_t K, int64_t lda,
+              const nqk_epilogue* p, bool f32x);  // nqk_pgemm.hip
+}
 
 static int num_cus() {
   static int n = 0;
@@ -1955,6 +1959,16 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     const bool f32x = i32 && (epi == EPI_QKV || (epi == EPI_GELU && e.gelu_filter)) && zp_small &&
                       16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
     const bool use_pp = pp && !params->b_packed;
+    // the persistent 16x16x64 GEMM (nqk_pgemm.hip) where it takes the case
+    if (params->bt_pg != nullptr) {
+      const bool f32x_r = i32 && epi == EPI_RESID && 16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
+      const int rc = pg_launch(epi, a, params->bt_pg, M, N, K, lda, params, f32x || f32x_r);
+      if (rc < 0) return rc;
+      if (rc == 1) {
+        g_last_gemm = 4;
+        return 0;
+      }
+    }
     // the persistent 256 x 256 kernel where it takes the shape: QKV by default; FFN-up +
     // GELU with NQK_PROJ_GELU=1 and the residual epilogues with NQK_PROJ_RESID=1 (faster
     // alone, not inside the two-stream forward, DESIGN.md "Projection GEMM variants");

@@ -1,0 +1,668 @@
+// k_pg: the round-3 persistent projection GEMM of the fused ViT layer (the hot loop of
+// numpy_quantization.py:44-61 q_matmul for every act x W MatMul, with the consumer chain of
+// model.py:486-565 in the epilogue: QKV head split + quantize, FFN-up + GELU + quantize,
+// out-projection / FFN-down + bias + residual).
+//
+// Why this shape (measured on MI355X, tools/micro/fill.hip, tools/micro/xwave.hip,
+// profiles/r03_*):
+//  * v_mfma_i32_16x16x64_i8 sustains 3.9 POPS on random operands against 3.26 for the
+//    32x32x32 form: the chip holds ~1.95 GHz under it instead of ~1.6 (same cycles per op).
+//  * A SIMD overlaps one wave's MFMAs with VALU work (its own or another wave's) up to
+//    ~4-6 VALU per 32x32x32-equivalent; past that the VALU issue (≈4 cycles each) sets
+//    the pace.  The epilogues are VALU work, so: two independent 4-wave workgroups per CU
+//    (128 x 256 tiles), the second started half a tile later, so that one workgroup's
+//    epilogue runs beside the other's k loop; and epilogues with fewer VALU per element
+//    (zero-point column term as the MFMA's initial accumulator, one fma for the QKV
+//    rescale, a single measure per element for the rounding filter).
+//
+// Layout: 4 waves side by side along N, each 128 rows x 64 columns = 8 x 4 MFMA tiles of
+// 16 x 16 (acc[i][j], 4 registers).  The products are computed transposed (Bt fragment as
+// the MFMA's A operand), and the weight image stores the 64 columns of a wave permuted
+// (bperm), so that lane l holds, for M-subtile i, row 16 i + (l & 15) and the 16
+// CONSECUTIVE columns 16 (l >> 4) + 4 j + r: one 16-byte store per subtile (int8 outputs)
+// or four (f32), straight from the accumulators.
+// A [M][K] int8 (activations) and the tile-packed weight image both go HBM/L2 -> LDS by
+// buffer LDS-DMA into a 3-stage ring (24 KiB per 64-deep k-step); the 16-B chunks are
+// XOR-swizzled (sw) so the fragment reads are conflict-free ds_read_b128.  Every VMEM
+// operation of the loop is counted by compile-time vmcnt waits; LDS reads are inline asm
+// (a compiler-visible read of LDS-DMA'd bytes gets a vmcnt(0) that would drain the ring).
+#include <type_traits>
+
+#include "nqk_common.h"
+#include "nqk_numerics.h"
+
+namespace nqk {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int PG_BM = 128, PG_BN = 256, PG_BK = 64, PG_RD = 3;
+constexpr int PG_ASTG = PG_BM * PG_BK;           // 8 KiB
+constexpr int PG_STG = PG_ASTG + PG_BN * PG_BK;  // 24 KiB
+constexpr int PG_COLP = PG_RD * PG_STG;          // 2 slots x (ct[256] int32 | bias[256] f32)
+constexpr int PG_LDS = PG_COLP + 2 * 2048;       // 76 KiB: two workgroups per CU
+constexpr int PG_PW = 2 + 4;                      // LDS-DMA pieces per wave per stage
+
+enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fused.hip
+
+#ifndef NQK_PG_DIAG
+#define NQK_PG_DIAG 0  // diagnostic builds only (tools/pg_diag.sh): 1 = no epilogue stores,
+                       // 2 = trivial epilogue math, 4 = no operand loads, 8 = no barriers,
+                       // 16 = no fragment reads
+#endif
+
+// physical 16-B chunk of logical chunk c in 64-B LDS row r is c ^ pg_sw(r): the 16 lanes of
+// each ds_read_b128 lane group (rows 16 i + (l & 15), chunk l >> 4) then hit 16 different
+// 4-bank slots
+__host__ __device__ constexpr int pg_sw(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+// column (within the wave's 64) held by the wave's LDS B row rw = 16 j + c.  Layout 0 (int8
+// outputs): lane (l & 15, lg = l >> 4) gets columns 16 lg + 4 j + r, 16 consecutive bytes;
+// layout 1 (f32 outputs): columns 16 j + 4 lg + r, so each 16-B store instruction j covers
+// 64 contiguous bytes of a row with the 4 lanes of that row
+__host__ __device__ constexpr int pg_bperm(int rw, int layout) {
+  return layout == 0 ? 16 * ((rw & 15) >> 2) + 4 * (rw >> 4) + (rw & 3) : rw;
+}
+
+template <int I>
+using ic = std::integral_constant<int, I>;
+template <int B, int E, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(ic<B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+__device__ __forceinline__ rsrc_t pg_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void pg_dma16(rsrc_t r, void* l, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)l, 16, voff, soff, 0, 0);
+}
+// LDS reads are compiler-visible (it places the lgkmcnt waits; an async load's destination
+// register must never be copied before its wait, which only the compiler can guarantee);
+// the compiler does not order them behind LDS-DMA, the explicit vmcnt waits + barriers do
+__device__ __forceinline__ v4i pg_lds16(const void* p) {
+  return *reinterpret_cast<const v4i*>(p);  // p points into the kernel's LDS array: ds_read_b128
+}
+// ds_read_b128 at base + a compile-time byte offset (the instruction's 16-bit offset field:
+// one address VGPR for every fragment read of the loop)
+#ifndef NQK_PG_ASMREAD
+#define NQK_PG_ASMREAD 0  // diagnostic: fragment reads by inline asm
+#endif
+template <int OFF>
+__device__ __forceinline__ v4i pg_lds16o(const int8_t* base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds_read offset");
+  if constexpr (NQK_PG_ASMREAD) {
+    v4i v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)base), "n"(OFF));
+    return v;
+  } else {
+    return *reinterpret_cast<const v4i*>(base + OFF);  // the offset folds into the instruction
+  }
+}
+__device__ __forceinline__ void pg_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// lgkmcnt(0) that the values read by pg_lds16 pass through: their uses cannot be moved
+// above the wait (a plain wait orders only memory operations)
+__device__ __forceinline__ void pg_lgkm_tie(v4i& a, v4i& b, v4i& c, v4i& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void pg_lgkm_tie8(v4i (&a)[4], v4i (&b)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+__device__ __forceinline__ void pg_vmcnt_tie(v4u (&a)[4]) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : "n"(N > 63 ? 63 : N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+__device__ __forceinline__ void pg_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N > 63 ? 63 : N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// 16-byte buffer load to VGPRs (compiler-visible: it places the vmcnt wait before the use)
+__device__ __forceinline__ v4u pg_load16(rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+}
+
+struct PgEpi {
+  float sacc[3];      // dequant scale per column group
+  float rsf[3];       // RN32(1 / s_out)
+  float c1[3];        // RN32(sacc * rsf)            (QKV fast path)
+  float k1[3];        // |c1| 2^-21                  (QKV filter: rounding error per |v|)
+  float zp128[3];     // zp_out + 128 (f32)
+  float s_out[3];
+  double rs_out[3], zp_out[3];
+  void* out[3];
+  const float* bias;
+  const float* resid;
+  const int32_t* colterm;  // col[n] * zpa (int32)
+  float lo128, hi128;
+  double lo, hi;
+  int group_cols, tokens, heads, hdim;
+  float g_rel, g_lim;  // GELU filter (nqk_fused.hip make_epi)
+  float div, add1, mul2;
+  double rdiv;
+  int ldo;  // row stride (elements) of the GELU / RESID output
+};
+
+// quantize (numpy_quantization.py:24-34) with f64 zero-point add and clipping
+__device__ __forceinline__ int pg_quant_exact(float x, float s, double rs, double zp, double lo, double hi) {
+  (void)s;
+  const float t = (float)((double)x * rs);  // RN32(x / s) (s normal, host-checked)
+  const double u = zp + (double)t;
+  return (int)__builtin_rint(__builtin_fmin(__builtin_fmax(u, lo), hi));
+}
+
+// Q_LIM = (0.5 - 2^-126)(1 - 2^-23) rounded down: a rounded fma measure below it keeps the
+// exact one below 0.5 - 2^-126 (nqk_fused.hip quant_filter)
+constexpr float PG_QLIM = 0x1.fffffcp-2f;
+
+template <int EPI, int NK, bool F32X>
+__global__ void __launch_bounds__(256, 2)
+k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
+     int stagger, PgEpi e) {
+  static_assert(NK % PG_RD == 0 && NK >= 2 * PG_RD, "k_pg: NK a multiple of the ring depth");
+  constexpr bool RESID = EPI == PG_RESID;
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l15 = lane & 15, lg = lane >> 4;
+
+  // tiles: the workgroups with blockIdx % 8 == x (one XCD under round-robin placement)
+  // walk the band [lo, hi) of tile ids, every nx-th tile from lo + jx; tile ids are
+  // row-panel major, so the tiles in flight on an XCD share A row panels in its L2
+  const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X, jx = blockIdx.x / X;
+  const int nx = (G - x + X - 1) / X;
+  const int lo = (int)((int64_t)ntiles * x / X), hi = (int)((int64_t)ntiles * (x + 1) / X);
+  const int first = lo + jx;
+  if (first >= hi) return;
+  const int cnt = (hi - first + nx - 1) / nx;
+  // the second workgroup of a CU (under round-robin placement: blockIdx >= G / 2) starts
+  // about half a tile later, so that the two workgroups' epilogues do not coincide
+  if (stagger > 0 && (int)blockIdx.x >= G / 2)
+    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(8);  // ~512 cycles each
+
+  constexpr int64_t BSTRIDE = (int64_t)NK * PG_BN * PG_BK;  // bytes of one column panel
+  const rsrc_t r_a = pg_rsrc(A, (uint32_t)((uint64_t)M * lda));
+  const rsrc_t r_b = pg_rsrc(Bp, (uint32_t)((uint64_t)tiles_n * BSTRIDE));
+  // LDS-DMA sources: A piece pp of wave w = rows 32 w + 16 pp + (l >> 2), physical chunk l & 3
+  const uint32_t va = (uint32_t)((32 * wave + (lane >> 2)) * lda + 16 * ((lane & 3) ^ pg_sw(lane >> 2)));
+  const uint32_t vb = (uint32_t)(4096 * wave + 16 * lane);
+  // fragment offsets: row (l & 15) of a 16-row subtile, logical chunk l >> 4
+  const int f_off = l15 * 64 + 16 * (lg ^ pg_sw(l15));
+
+  struct Src { uint32_t sa, sb; int r0, tn; };
+  auto src_of = [&](int tile) __attribute__((always_inline)) {
+    Src s;
+    const int tm = tile / tiles_n;
+    s.tn = tile - tm * tiles_n;
+    // a ragged last tile row is computed as rows M - 128 .. M - 1 (the rows it shares
+    // with the tile above are written twice with the same values; host: out != resid)
+    s.r0 = tm * PG_BM < M - PG_BM ? tm * PG_BM : M - PG_BM;
+    s.sa = (uint32_t)s.r0 * (uint32_t)lda;
+    s.sb = (uint32_t)((int64_t)s.tn * BSTRIDE);
+    return s;
+  };
+  auto issue_stage = [&](const Src& s, int kt, int slot) __attribute__((always_inline)) {
+    if constexpr ((NQK_PG_DIAG & 4) != 0) return;
+    int8_t* st = lds + slot * PG_STG;
+    pg_dma16(r_a, st + (2 * wave) * 1024, va, s.sa + kt * PG_BK);
+    pg_dma16(r_a, st + (2 * wave + 1) * 1024, va, s.sa + 16u * (uint32_t)lda + kt * PG_BK);
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      pg_dma16(r_b, st + PG_ASTG + (4 * wave + p) * 1024, vb, s.sb + (uint32_t)(kt * (PG_BN * PG_BK) + p * 1024));
+  };
+  // column constants of a tile (ct[256] | bias[256], 2 KiB): wave w moves bytes
+  // [512 w, 512 w + 512) with lanes 0..31 (one VMEM operation per wave, like every wave)
+  const rsrc_t r_ct = pg_rsrc(e.colterm, (uint32_t)((uint64_t)N * 4));
+  const rsrc_t r_bias = pg_rsrc(e.bias, e.bias ? (uint32_t)((uint64_t)N * 4) : 0u);
+  auto issue_colp = [&](int tn, int cslot) __attribute__((always_inline)) {
+    int8_t* dst = lds + PG_COLP + cslot * 2048 + wave * 512;
+    const uint32_t voff = (uint32_t)((tn * PG_BN + (wave & 1) * 128 + (lane & 31) * 4) * 4);
+    if (lane < 32) {
+      if (wave < 2) pg_dma16(r_ct, dst, voff, 0);
+      else pg_dma16(r_bias, dst, voff, 0);  // bias == null: the descriptor returns zeros
+    }
+  };
+
+  v4i acc[8][4];
+  v4i a_lo[4], a_hi[4], b0[4], b1[4];
+  const int8_t* const fa_base = lds + f_off;
+  const int8_t* const fb_base = fa_base + 4096 * wave;
+  // fragment reads: A subtile i (rows 16 i ..), B subtile j of the wave (rows 64 w + 16 j ..)
+  auto rd_a = [&](v4i (&dst)[4], auto SLOT, auto I0, auto Q) __attribute__((always_inline)) {
+    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
+    constexpr int q = decltype(Q)::value;
+    dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + (decltype(I0)::value + q) * 1024>(fa_base);
+  };
+  auto rd_b = [&](v4i (&dst)[4], auto SLOT, auto Q) __attribute__((always_inline)) {
+    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
+    constexpr int q = decltype(Q)::value;
+    dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + PG_ASTG + q * 1024>(fb_base);
+  };
+  // 16 MFMAs of one half step (M-subtiles 4 h .. 4 h + 3) with fn(q) after MFMA q
+  auto half = [&](auto H, auto FIRST, const v4i (&aa)[4], const v4i (&bb)[4], const v4i (&ci)[4], auto&& fn)
+      __attribute__((always_inline)) {
+    constexpr int h = decltype(H)::value;
+    sfor<0, 16>([&](auto Q) __attribute__((always_inline)) {
+      constexpr int q = decltype(Q)::value, ii = q >> 2, j = q & 3;
+      if constexpr (decltype(FIRST)::value)
+        acc[4 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], ci[j], 0, 0, 0);
+      else
+        acc[4 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], acc[4 * h + ii][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      fn(Q);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
+  // ---------------------------------------------------------------- epilogue of a tile
+  // rows r0 + 16 i + (l & 15), columns n0 + 64 w + 16 (l >> 4) + 0..15
+  auto epilogue = [&](const Src& s, int cslot) __attribute__((always_inline)) {
+    const int n0 = s.tn * PG_BN;
+    const int cw = n0 + 64 * wave;  // the wave's 64 columns: one head, one column group (host)
+    const int col0 = cw + 16 * lg;
+    const int8_t* cp = lds + PG_COLP + cslot * 2048;
+    float bias[16];
+    {
+      v4i bb[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bb[g] = pg_lds16(cp + 1024 + (64 * wave + 16 * lg + 4 * g) * 4);
+      pg_lgkm_tie(bb[0], bb[1], bb[2], bb[3]);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) bias[q] = __int_as_float(bb[q >> 2][q & 3]);
+    }
+    {
+      int g3 = 0;
+      if constexpr (EPI == PG_QKV) {
+        g3 = cw / e.group_cols;
+        g3 = g3 > 2 ? 2 : g3;
+      }
+      const float sacc = g3 == 0 ? e.sacc[0] : (g3 == 1 ? e.sacc[1] : e.sacc[2]);
+      const float rsf = g3 == 0 ? e.rsf[0] : (g3 == 1 ? e.rsf[1] : e.rsf[2]);
+      const float c1 = g3 == 0 ? e.c1[0] : (g3 == 1 ? e.c1[1] : e.c1[2]);
+      const float k1 = g3 == 0 ? e.k1[0] : (g3 == 1 ? e.k1[1] : e.k1[2]);
+      const float zp128 = g3 == 0 ? e.zp128[0] : (g3 == 1 ? e.zp128[1] : e.zp128[2]);
+      const float s_out = g3 == 0 ? e.s_out[0] : (g3 == 1 ? e.s_out[1] : e.s_out[2]);
+      const double rs_out = g3 == 0 ? e.rs_out[0] : (g3 == 1 ? e.rs_out[1] : e.rs_out[2]);
+      const double zp = g3 == 0 ? e.zp_out[0] : (g3 == 1 ? e.zp_out[1] : e.zp_out[2]);
+      void* op = g3 == 0 ? e.out[0] : (g3 == 1 ? e.out[1] : e.out[2]);
+      // QKV: the head-layout buffer holds whole images, ceil(M / tokens) of them
+      const rsrc_t r_out = pg_rsrc(
+          op, (uint32_t)(EPI == PG_QKV ? (uint64_t)((M + e.tokens - 1) / e.tokens) * e.tokens * e.heads * e.hdim
+                                       : (uint64_t)M * e.ldo));
+      // QKV: u = v c1 + c2 with c2 = RN(bias rsf): within |v| k1 + kb of zp + 128 + t,
+      // t = RN(RN(RN(v sacc) + bias) / s_out) (DESIGN.md §4.3 error bound); kb from the
+      // lane's largest |c2|, folded into the lane's limit
+      float c2[16];
+      float lim = PG_QLIM;
+      if constexpr (EPI == PG_QKV) {
+        float cm = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          c2[q] = bias[q] * rsf;
+          cm = __builtin_fmaxf(cm, __builtin_fabsf(c2[q]));
+        }
+        lim = (PG_QLIM - cm * 0x1p-20f) - 0x1p-22f;  // conservative: every rounding down
+      } else {
+        lim = e.g_lim;
+      }
+      int hh = 0;
+      if constexpr (EPI == PG_QKV) hh = (cw - g3 * e.group_cols) / e.hdim;
+      sfor<0, 8>([&](auto I) __attribute__((always_inline)) {
+        constexpr int i = decltype(I)::value;
+        const int m = s.r0 + 16 * i + l15;
+        uint32_t off;
+        if constexpr (EPI == PG_QKV) {
+          const int img = m / e.tokens, t = m - img * e.tokens;
+          off = (uint32_t)(((img * e.heads + hh) * e.tokens + t) * e.hdim + 16 * lg);
+        } else {
+          off = (uint32_t)(m * e.ldo + col0);
+        }
+        uint32_t pk[4] = {0, 0, 0, 0};
+        uint32_t worst = 0;
+        float hv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int a = acc[i][q >> 2][q & 3];
+          const float vf = (float)a;
+          float u;
+          if constexpr ((NQK_PG_DIAG & 2) != 0) {
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32((float)(a & 255), q & 3, pk[q >> 2]);
+            continue;
+          }
+          if constexpr (EPI == PG_QKV) {
+            u = __builtin_fmaf(vf, c1, c2[q]);
+            const float r = __builtin_rintf(u);
+            const float meas = __builtin_fmaf(__builtin_fabsf(vf), k1, __builtin_fabsf(u - r));
+            worst = __builtin_elementwise_max(worst, __float_as_uint(meas));
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, e.lo128, e.hi128), q & 3,
+                                                        pk[q >> 2]);
+          } else {  // GELU: h exactly as the reference (F32X), then the filtered fast chain
+            const float h = bias[q] + vf * sacc;
+            hv[q] = h;
+            const float tf = gelu_fast(h) * rsf;
+            const float r = __builtin_rintf(tf);
+            const float meas = __builtin_fmaf(__builtin_fabsf(h), e.g_rel, __builtin_fabsf(tf - r));
+            worst = __builtin_elementwise_max(worst, __float_as_uint(meas));
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, e.lo128, e.hi128), q & 3,
+                                                        pk[q >> 2]);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pk[g] ^= 0x80808080u;
+        if constexpr ((NQK_PG_DIAG & 2) == 0) {
+          if (__builtin_expect(__any(worst >= __float_as_uint(lim)), 0)) {
+            // the exact chain for every element the filter could not decide
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const int a = acc[i][q >> 2][q & 3];
+              const float vf = (float)a;
+              bool slow;
+              if constexpr (EPI == PG_QKV) {
+                const float u = __builtin_fmaf(vf, c1, c2[q]);
+                const float r = __builtin_rintf(u);
+                slow = !(__builtin_fmaf(__builtin_fabsf(vf), k1, __builtin_fabsf(u - r)) < lim);
+              } else {
+                const float tf = gelu_fast(hv[q]) * rsf;
+                const float r = __builtin_rintf(tf);
+                slow = !(__builtin_fmaf(__builtin_fabsf(hv[q]), e.g_rel, __builtin_fabsf(tf - r)) < lim);
+              }
+              if (__any(slow)) {
+                if (slow) {
+                  float y = bias[q] + vf * sacc;  // F32X: the f64 dequantize, exactly
+                  if constexpr (EPI == PG_GELU) {
+                    const float aa = ref_erf((float)((double)y * e.rdiv)) + e.add1;
+                    y = (y * aa) * e.mul2;
+                  }
+                  const int qv = pg_quant_exact(y, s_out, rs_out, zp, e.lo, e.hi);
+                  pk[q >> 2] = (pk[q >> 2] & ~(0xffu << (8 * (q & 3)))) | ((uint32_t)(qv & 0xff) << (8 * (q & 3)));
+                }
+              }
+            }
+          }
+        }
+        const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
+        if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
+        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, off, 0, 0);
+      });
+    }
+  };
+
+  // RESID epilogue: y = (bias + RN(v sacc)) + residual, f32 stores.  The residual rows of
+  // subtile i are loaded by 4 untracked 16-B loads (res_issue); subtiles 0 and 1 are issued
+  // before the next tile's stages (so waiting for them does not wait for the stages)
+  const rsrc_t r_res = pg_rsrc(RESID ? e.resid : nullptr, RESID ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
+  v4u resv[3][4];
+  auto res_issue = [&](const Src& s, auto I) __attribute__((always_inline)) {
+    constexpr int i = decltype(I)::value;
+    const uint32_t o = (uint32_t)(((s.r0 + 16 * i + l15) * e.ldo + s.tn * PG_BN + 64 * wave + 4 * lg) * 4);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) resv[i % 3][g] = pg_load16(r_res, o + 64 * g, 0u);
+  };
+  auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
+    const int8_t* cp = lds + PG_COLP + cslot * 2048;
+    float bias[16];
+    {
+      v4i bb[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bb[g] = pg_lds16(cp + 1024 + (64 * wave + 16 * g + 4 * lg) * 4);
+      pg_lgkm_tie(bb[0], bb[1], bb[2], bb[3]);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) bias[q] = __int_as_float(bb[q >> 2][q & 3]);
+    }
+    const rsrc_t r_out = pg_rsrc(e.out[0], (uint32_t)((uint64_t)M * e.ldo * 4));
+    const float sacc = e.sacc[0];
+    sfor<0, 8>([&](auto I) __attribute__((always_inline)) {
+      constexpr int i = decltype(I)::value;
+      // (the compiler waits for subtile i's residual: its loads are visible to it)
+      const v4u(&rv)[4] = resv[i % 3];
+      const uint32_t o = (uint32_t)(((s.r0 + 16 * i + l15) * e.ldo + s.tn * PG_BN + 64 * wave + 4 * lg) * 4);
+      float y[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int a = acc[i][q >> 2][q & 3];
+        const float d = F32X ? (float)a * sacc : (float)((double)a * (double)sacc);
+        y[q] = (bias[q] + d) + __uint_as_float(rv[q >> 2][q & 3]);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const v4u st = v4u{__float_as_uint(y[4 * g]), __float_as_uint(y[4 * g + 1]), __float_as_uint(y[4 * g + 2]),
+                           __float_as_uint(y[4 * g + 3])};
+        if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
+        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, o + 64 * g, 0, 0);
+      }
+      if constexpr (i + 2 < 8) res_issue(s, ic<i + 2>{});
+    });
+  };
+
+  // ---------------------------------------------------------------- the persistent loop
+  // VMEM operations per wave, in issue order: [colp(next)] at step 1; stage kt + 2 in step
+  // kt's first half; after the k loop (RESID: residual of subtiles 0, 1), the next tile's
+  // stages 0 and 1, then the epilogue's operations (EOPS)
+  // RESID: 8 x 4 stores after the stages (counted conservatively without the 6 x 4 residual
+  // loads, which the compiler may hoist above the stage issues: a smaller count only waits more)
+  constexpr int EOPS = RESID ? 32 : 8;
+  Src cur = src_of(first);
+  issue_colp(cur.tn, 0);
+  issue_stage(cur, 0, 0);
+  issue_stage(cur, 1, 1);
+  for (int it = 0; it < cnt; ++it) {
+    const bool more = it + 1 < cnt;
+    const Src nxt = src_of(first + (more ? it + 1 : it) * nx);
+    const int cs = it & 1;
+    // stage 0 and this tile's column constants landed (younger: stage 1, the previous
+    // epilogue's operations)
+    if (it == 0) pg_vmcnt<PG_PW>();
+    else pg_vmcnt<PG_PW + EOPS>();
+    if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // initial accumulators: minus the zero-point column terms of the lane's 16 columns
+    v4i cinit[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      cinit[j] = pg_lds16(lds + PG_COLP + cs * 2048 + (64 * wave + (RESID ? 16 * j + 4 * lg : 16 * lg + 4 * j)) * 4);
+    sfor<0, 4>([&](auto Q) __attribute__((always_inline)) {
+      rd_a(a_lo, ic<0>{}, ic<0>{}, Q);
+      rd_b(b0, ic<0>{}, Q);
+    });
+    pg_lgkm_tie8(a_lo, b0);
+    pg_lgkm_tie(cinit[0], cinit[1], cinit[2], cinit[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cinit[j] = -cinit[j];
+    sfor<0, NK>([&](auto KT) __attribute__((always_inline)) {
+      constexpr int kt = decltype(KT)::value;
+      constexpr int slot = kt % PG_RD;
+      v4i(&bc)[4] = (kt & 1) ? b1 : b0;
+      v4i(&bn)[4] = (kt & 1) ? b0 : b1;
+      if constexpr (kt > 0) pg_lgkm_tie8(a_lo, bc);  // this step's fragments (read in step kt - 1)
+      // first half: subtiles 0..3; between the MFMAs the second half's A fragments and the
+      // refill of the slot step kt - 1 read (stage kt + 2)
+      half(ic<0>{}, std::integral_constant<bool, kt == 0>{}, a_lo, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
+        constexpr int q = decltype(Q)::value;
+        if constexpr (q < 4) rd_a(a_hi, ic<slot>{}, ic<4>{}, Q);
+        if constexpr (q == 4 && kt + 2 < NK) issue_stage(cur, kt + 2, (kt + 2) % PG_RD);
+      });
+      if constexpr (kt == 1) issue_colp(nxt.tn, cs ^ 1);
+      if constexpr (kt + 1 < NK) {
+        // stage kt + 1 landed; younger: stage kt + 2 (if issued), colp (step 1), and for
+        // stage 1 the previous tile's epilogue operations
+        constexpr int y = (kt + 2 < NK ? PG_PW : 0) + ((kt == 1 || kt == 2) ? 1 : 0);
+        if (kt == 0 && it > 0) pg_vmcnt<y + EOPS>();
+        else pg_vmcnt<y>();
+        pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
+        if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
+      }
+      half(ic<1>{}, std::integral_constant<bool, kt == 0>{}, a_hi, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
+        constexpr int q = decltype(Q)::value;
+        if constexpr (kt + 1 < NK) {
+          if constexpr (q < 4) rd_a(a_lo, ic<(kt + 1) % PG_RD>{}, ic<0>{}, Q);
+          else if constexpr (q < 8) rd_b(bn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
+        }
+      });
+    });
+    // RESID: the residual rows of the first two subtiles, then the next tile's first
+    // stages (slots 0 and 1: last read before step NK - 2's barrier)
+    if constexpr (RESID) {
+      res_issue(cur, ic<0>{});
+      res_issue(cur, ic<1>{});
+    }
+    // (the last tile re-stages its own first stages: never read, drained at the end; the
+    // VMEM counts stay the same on every path)
+    issue_stage(nxt, 0, 0);
+    issue_stage(nxt, 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RESID) epilogue_resid(cur, cs);
+    else epilogue(cur, cs);
+    cur = nxt;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// weight image of k_pg: [N / 256][K / 64] stages of 256 rows x 64 B in the LDS order of the
+// stage (row rho: column 64 (rho >> 6) + pg_bperm(rho & 63) of the panel; physical chunk
+// pc: logical chunk pc ^ pg_sw(rho)); columns past N are zero
+__global__ void k_pack_pg(const int8_t* __restrict__ bt, int8_t* __restrict__ out, int64_t N, int64_t K, int64_t ldb,
+                          int64_t chunks, int layout) {
+  const int64_t nk = K / PG_BK;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < chunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t blk = c >> 10, w = c & 1023;
+    const int64_t tn = blk / nk, kt = blk - tn * nk;
+    const int rho = (int)(w >> 2), pc = (int)(w & 3);
+    const int64_t col = tn * PG_BN + 64 * (rho >> 6) + pg_bperm(rho & 63, layout);
+    const int lc = pc ^ pg_sw(rho);
+    int4 v = make_int4(0, 0, 0, 0);
+    if (col < N) v = *reinterpret_cast<const int4*>(bt + col * ldb + kt * PG_BK + lc * 16);
+    reinterpret_cast<int4*>(out)[c] = v;
+  }
+}
+
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ host
+extern "C" int nqk_pack_pg(const int8_t* bt, int8_t* out, int64_t N, int64_t K, int64_t ldb, int layout) {
+  if (N <= 0 || K <= 0) return 0;
+  if (layout != 0 && layout != 1) return fail("nqk_pack_pg: layout must be 0 (int8 outputs) or 1 (f32 outputs)");
+  if (K % PG_BK) return fail("nqk_pack_pg: K must be a multiple of 64");
+  if ((((uintptr_t)bt) & 15) || (ldb & 15) || (((uintptr_t)out) & 15)) return fail("nqk_pack_pg: unaligned operand");
+  const int64_t chunks = (N + PG_BN - 1) / PG_BN * PG_BN * K / 16;
+  hipLaunchKernelGGL(k_pack_pg, dim3(grid_for(chunks)), dim3(kThreads), 0, stream(), bt, out, N, K, ldb, chunks, layout);
+  return launch_status("nqk_pack_pg");
+}
+
+static int pg_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// Launches k_pg for one projection GEMM when it takes the case; returns 1 if launched, 0
+// if the caller must use another kernel, < 0 on error.  bp: the nqk_pack_pg image.
+int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, int64_t K, int64_t lda,
+              const nqk_epilogue* p, bool f32x) {
+  if (getenv("NQK_NO_PG")) return 0;
+  if (bp == nullptr || p->colterm == nullptr || p->b_packed == 2) return 0;
+  if (!(epi == PG_QKV || epi == PG_RESID || epi == PG_GELU)) return 0;
+  if (!(K == 768 || K == 3072) || N % PG_BN != 0 || M < PG_BM) return 0;
+  if ((double)M * N * 4.0 >= 4294967295.0 || (double)M * lda >= 4294967295.0) return 0;
+  if ((epi == PG_QKV || epi == PG_GELU) && (!f32x || K != 768)) return 0;
+  if (epi == PG_QKV && !(p->hdim == 64 && p->group_cols % 64 == 0 && (double)M * p->heads * p->hdim < 2147483647.0))
+    return 0;
+  // the residual epilogues stay on k_qgemm_big unless NQK_PG_RESID=1 (k_pg measured slower
+  // there: profiles/r03_pg_micro.txt)
+  if (epi == PG_RESID && (!getenv("NQK_PG_RESID") || p->resid == nullptr || (M % PG_BM != 0 && p->resid == p->out[0])))
+    return 0;
+  if (epi == PG_GELU && !(p->div == 1.41421354f && p->add1 == 1.0f && p->mul2 == 0.5f)) return 0;
+  auto al16 = [](const void* q) { return q == nullptr || (((uintptr_t)q) & 15) == 0; };
+  if (!al16(p->out[0]) || !al16(p->out[1]) || !al16(p->out[2]) || !al16(p->resid) || !al16(p->colterm) ||
+      !al16(p->bias) || !al16(a) || (lda & 15))
+    return 0;
+  if (p->bit_width != 8) return 0;  // the byte clamp by med3 + v_cvt_pk_u8 assumes [-128, 127]
+  PgEpi e{};
+  const int ng = epi == PG_QKV ? 3 : 1;
+  for (int g = 0; g < 3; ++g) {
+    const int gg = g < ng ? g : 0;
+    const float s_out = p->s_out[gg];
+    e.sacc[g] = p->s_acc[gg];
+    e.s_out[g] = s_out;
+    e.rs_out[g] = 1.0 / (double)s_out;
+    e.zp_out[g] = (double)p->zp_out[gg];
+    e.rsf[g] = s_out != 0.0f ? (float)(1.0 / (double)s_out) : 0.0f;
+    e.c1[g] = e.sacc[g] * e.rsf[g];
+    e.k1[g] = __builtin_fabsf(e.c1[g]) * 0x1p-21f;
+    e.zp128[g] = (float)p->zp_out[gg] + 128.0f;
+    e.out[g] = p->out[gg];
+    if (epi != PG_RESID) {
+      if (!(__builtin_fabsf(s_out) >= 0x1p-100f && __builtin_fabsf(s_out) <= 0x1p100f)) return 0;
+      if (p->zp_out[gg] < -(1 << 20) || p->zp_out[gg] > (1 << 20)) return 0;
+    }
+  }
+  e.bias = p->bias;
+  e.resid = p->resid;
+  e.colterm = p->colterm;
+  e.lo = -128.0;
+  e.hi = 127.0;
+  e.lo128 = 0.0f;
+  e.hi128 = 255.0f;
+  e.group_cols = p->group_cols > 0 ? p->group_cols : (int)N;
+  e.tokens = p->tokens;
+  e.heads = p->heads;
+  e.hdim = p->hdim;
+  e.div = p->div;
+  e.rdiv = 1.0 / (double)p->div;
+  e.add1 = p->add1;
+  e.mul2 = p->mul2;
+  e.ldo = (int)N;
+  if (epi == PG_GELU) {
+    // the GELU filter of nqk_fused.hip make_epi: |gelu_fast - gelu| <= GELU_REL |h| +
+    // GELU_ABS, plus the product t = y * rsf
+    const double ars = __builtin_fabs(1.0 / (double)p->s_out[0]) * 1.02;
+    e.g_rel = (float)((double)GELU_REL * 1.27 * ars);
+    const float g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
+    e.g_lim = (float)((0.5 - (double)g_abs) * (1.0 - 0x1p-22));
+  }
+  const int tiles_n = (int)(N / PG_BN), tiles_m = (int)((M + PG_BM - 1) / PG_BM);
+  const int nt = tiles_m * tiles_n;
+  const int slots = 2 * pg_num_cus();
+  const int grid = nt < slots ? nt : slots;
+  // initial delay of the second workgroup per CU, in units of s_sleep 8 (~512 cycles)
+  const char* sv = getenv("NQK_PG_STAGGER");
+  const int stg = grid == slots ? (sv ? atoi(sv) : 0) : 0;
+  const int key = epi * 4 + (K == 3072 ? 2 : 0) + (f32x ? 1 : 0);
+  switch (key) {
+#define PGL(E, NKV, X)                                                                                          \
+  case E * 4 + (NKV == 48 ? 2 : 0) + (X ? 1 : 0):                                                               \
+    hipLaunchKernelGGL((k_pg<E, NKV, X>), dim3(grid), dim3(256), PG_LDS, stream(), a, bp, (int)M, (int)N, (int)lda, \
+                       tiles_n, nt, stg, e);                                                                    \
+    break;
+    PGL(PG_QKV, 12, true)
+    PGL(PG_GELU, 12, true)
+    PGL(PG_RESID, 12, true) PGL(PG_RESID, 12, false) PGL(PG_RESID, 48, true) PGL(PG_RESID, 48, false)
+#undef PGL
+    default:
+      return 0;
+  }
+  const int rc = launch_status("nqk_qgemm_fused(pg)");
+  return rc < 0 ? rc : 1;
+}
+
+}  // namespace nqk

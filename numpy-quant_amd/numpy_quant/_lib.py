@@ -33,7 +33,7 @@ class Epilogue(ctypes.Structure):
                 ("s_acc", ctypes.c_float * 3), ("s_out", ctypes.c_float * 3), ("zp_out", ctypes.c_int64 * 3),
                 ("out", ctypes.c_void_p * 3), ("bias", ctypes.c_void_p), ("resid", ctypes.c_void_p),
                 ("div", ctypes.c_float), ("add1", ctypes.c_float), ("mul2", ctypes.c_float),
-                ("b_packed", ctypes.c_int32), ("colterm", ctypes.c_void_p)]
+                ("b_packed", ctypes.c_int32), ("colterm", ctypes.c_void_p), ("bt_pg", ctypes.c_void_p)]
 
 
 class Attention(ctypes.Structure):
@@ -93,6 +93,7 @@ SIGNATURES = {
     "nqk_where_f32": [_p, _p, _p, _p, _i, _lp, _lp, _lp, _lp],
     "nqk_pack_b": [_p, _p, _l, _l, _l],
     "nqk_pack_b4": [_p, _p, _l, _l, _l],
+    "nqk_pack_pg": [_p, _p, _l, _l, _l, _i],
     "nqk_qgemm_fused": [_i, _p, _p, _l, _l, _l, _l, _l, _l, _lp, _l, _l, ctypes.POINTER(Epilogue)],
     "nqk_qgemm_last_kernel": [],
     "nqk_ln_quant": [_p, _p, _p, _p, _l, _l, _f, _f, _l, _i],

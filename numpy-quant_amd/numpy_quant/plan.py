@@ -468,7 +468,7 @@ class FusedEmbed:
                                              4 * (n * hw * self.kk + self.kk * self.kout + n * (hw + 1) * self.kout)),
                          unit="flop32")
         m.add.outputs[0].data = FTensor(out)
-        m.conv_out.data = None
+        m.conv_out.data = FusedAway(m.conv_out.name)
 
 
 # ----------------------------------------------------------------------------- Gather after LN
@@ -502,7 +502,7 @@ class LnGather:
         xs = x.take(self.g.inputs[1].data, axis=int(self.g.attrs.get("axis", 0)))
         args = [xs] + [qmodel._dequant_input(v) if isinstance(v.data, QTensor) else v.data for v in self.ln.inputs[1:]]
         self.g.outputs[0].data = onnx_operator_implementation("LayerNormalization", args, self.ln.attrs)[0]
-        self.ln.outputs[0].data = None
+        self.ln.outputs[0].data = FusedAway(self.ln.outputs[0].name)
 
 
 # ----------------------------------------------------------------------------- fused layer
@@ -545,6 +545,9 @@ class FusedLayer:
         # GEMM takes the shape
         self.bp = {k: _pack_b(b, self.bw) for k, b in (("qkv", self.bt_qkv), ("o", self.bt_o), ("1", self.bt_1),
                                                         ("2", self.bt_2))}
+        # the persistent 16x16x64 GEMM's weight images (nqk_pack_pg; used where it takes the case)
+        self.bpg = {k: _pack_pg(b, self.bw, lay) for k, b, lay in (("qkv", self.bt_qkv, 0), ("o", self.bt_o, 1),
+                                                                    ("1", self.bt_1, 0), ("2", self.bt_2, 1))}
         # max |column sum| of each weight: lets the GEMM epilogues prove f32 exactness
         self.cmax = {k: _absmax(c) for k, c in (("qkv", self.col_qkv), ("o", self.col_o), ("1", self.col_1),
                                                  ("2", self.col_2))}
@@ -576,9 +579,12 @@ class FusedLayer:
         return e
 
     def _b(self, e, key, bt):
-        """The B operand of a projection GEMM: its packed image if there is one."""
+        """The B operand of a projection GEMM: its packed image if there is one (and the
+        nqk_pack_pg image in e.bt_pg)."""
         bp = self.bp[key]
         e.b_packed = 0 if bp is None else bp[1]
+        pg = self.bpg[key]
+        e.bt_pg = None if pg is None else pg.ptr
         return bt if bp is None else bp[0]
 
     def _attention_unfused(self, w, B, T, Tp, H, Dh, D):
@@ -710,6 +716,19 @@ def _pack_b(bt, bit_width=8):
     return out, 1
 
 
+def _pack_pg(bt, bit_width=8, layout=0):
+    """The nqk_pack_pg image of a constant Bt [N][K] (int8 weights, K in {768, 3072},
+    N % 256 == 0; layout 0 for the int8-output epilogues QKV / GELU, 1 for the residual
+    epilogues), or None (NQK_NO_PG set, or a shape the persistent 16x16x64 GEMM does not
+    take)."""
+    N, K = bt.shape
+    if bit_width != 8 or K not in (768, 3072) or N % 256 or os.environ.get("NQK_NO_PG"):
+        return None
+    out = DeviceArray((N, K), np.int8)
+    _lib.call("nqk_pack_pg", bt.vp, out.vp, N, K, K, layout)
+    return out
+
+
 def _colterm(col, zpa):
     """col * zpa as an int32 device array, or None when a term leaves int32."""
     c = col.to_host().astype(np.int64) * int(zpa)
@@ -789,6 +808,22 @@ class Workspace:
         return self.bufs
 
 
+class FusedAway:
+    """The `.data` of a value computed inside a fused step during the last run (it never
+    left the step's kernels).  Reading it raises: run with `keep_values = True` to get every
+    intermediate (the reference's node loop fills them all, model.py:497-550)."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __getattr__(self, attr):
+        raise RuntimeError(f"value {self.name!r} was computed inside a fused plan step and not kept; "
+                           "set QModel.keep_values = True to read intermediates")
+
+    def __repr__(self):
+        return f"FusedAway({self.name!r})"
+
+
 class Plan:
     """Ordered steps: eager nodes and fused layers."""
 
@@ -851,9 +886,15 @@ class Plan:
                 placed.add(id(layer))
                 self.steps.append(("layer", layer))
                 self.fused += 1
+        # every value a fused step computes; each run first marks them all FusedAway, so that
+        # no tensor of an earlier run (eager, keep_values) can be read as if it were this
+        # run's; the steps then set the values their consumers outside the step read
+        self.internal = [v for node in qmodel.nodes if node in claimed for v in node.outputs]
 
     def run(self, qmodel, times=None, profile=False):
         streams = Streams(self.split, int(os.environ.get("NQK_STREAMS", "2")))
+        for v in self.internal:
+            v.data = FusedAway(v.name)
         try:
             for kind, obj in self.steps:
                 if kind == "node":

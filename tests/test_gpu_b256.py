@@ -5,10 +5,12 @@ ragged last tiles and XCD tile order at M = 50 432 rows).
 With fixed quantization parameters every op of the quantized forward is per image, so
   * image 0, the reference fixture's image, must give the reference's logits
     (tests/golden/vit_b1.npz, recorded from the reference's own QModel.__call__,
-    model.py:486-565) bit for bit, and
+    model.py:486-565) bit for bit,
+  * the WHOLE [256, 1000] output of the fused two-stream plan must equal one batch-256 run
+    of the node-by-node loop (keep_values=True: the reference's executor, pinned to the
+    reference by tests/test_gpu_models.py), and
   * the images at both ends of the two stream halves must equal a batch-1 run of the
-    same image through the node-by-node loop (itself pinned to the reference by
-    tests/test_gpu_models.py)."""
+    same image through the node-by-node loop."""
 import json
 import os
 
@@ -39,6 +41,14 @@ def _eager_rows(model, qmodel, x, rows):
         model.rebatch(B)
 
 
+def _eager_batch(qmodel, x):
+    qmodel.keep_values = True
+    try:
+        return qmodel([x])[0]
+    finally:
+        qmodel.keep_values = False
+
+
 def test_vit_b256_int8_matches_reference_fixture():
     from numpy_quant import onnx_proto
     from numpy_quant.model import Model
@@ -55,6 +65,7 @@ def test_vit_b256_int8_matches_reference_fixture():
     plan = qmodel._plan
     assert plan is not None and plan.split and plan.fused == 12 and plan.embeds == 1
     np.testing.assert_array_equal(out[0], arrs["bw8_out"][0])
+    np.testing.assert_array_equal(out, _eager_batch(qmodel, x), err_msg="fused B=256 vs node loop B=256")
     for i, ref in _eager_rows(model, qmodel, x, CHECK[1:]).items():
         np.testing.assert_array_equal(out[i], ref, err_msg=f"image {i}")
 
@@ -74,5 +85,6 @@ def test_vit_b256_int4_matches_batch1_node_loop():
     assert plan.fused == 12
     # the nibble-packed int4 weight images are in use
     assert all(layer.bp["1"][1] == 2 for kind, layer in plan.steps if kind == "layer")
+    np.testing.assert_array_equal(out, _eager_batch(qmodel, x), err_msg="fused B=256 vs node loop B=256")
     for i, ref in _eager_rows(model, qmodel, x, CHECK).items():
         np.testing.assert_array_equal(out[i], ref, err_msg=f"image {i}")

@@ -1,0 +1,119 @@
+"""The persistent 16x16x64 projection GEMM (k_pg, nqk_pgemm.hip) against the
+one-tile-per-workgroup 32x32x32 kernel (k_qgemm_big) on the same operands: bit-identical
+outputs for every epilogue (QKV head split + quantize, GELU + quantize, bias + residual
+with the f32 and the f64 dequantize), with many tiles per workgroup, with one, and with
+ragged last tile rows.  Small output scales put many values next to rounding boundaries, so
+the rounding filters' exact fallbacks run.  Reference: numpy_quantization.py:44-61 (q_matmul)
+and the consumer chains of model.py:486-565, pinned to the reference's fixtures through
+k_qgemm_big (tests/test_gpu_models.py, tests/test_gpu_b256.py)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _last_kernel():
+    from numpy_quant import _lib
+    return _lib.load().nqk_qgemm_last_kernel()
+
+
+def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed):
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_GELU, EPI_QKV, EPI_RESID, _gemm, _pack_b, _pack_pg
+    epi = {"qkv": EPI_QKV, "resid": EPI_RESID, "gelu": EPI_GELU}[epi_name]
+    rng = np.random.default_rng(seed)
+    a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
+    bt_h = rng.integers(-24, 25, size=(N, K), dtype=np.int8)
+    bt = DeviceArray.from_host(bt_h)
+    col_h = bt_h.astype(np.int64).sum(axis=1)
+    col = DeviceArray.from_host(col_h)
+    bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
+    resid = DeviceArray.from_host(rng.standard_normal((M, N)).astype(np.float32))
+    packed, kind = _pack_b(bt, 8)
+    pg = _pack_pg(bt, 8, 1 if epi == EPI_RESID else 0)
+    assert pg is not None
+    zpa = -5
+    colterm = DeviceArray.from_host((col_h * zpa).astype(np.int32))
+    for k in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_NO_PG"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("NQK_NO_PROJ", "1")
+    monkeypatch.setenv("NQK_PG_RESID", "1")  # opt-in for the residual epilogues
+    if no_f32x:
+        monkeypatch.setenv("NQK_NO_F32X", "1")
+    e = _lib.Epilogue()
+    e.zp_flags, e.bit_width = _lib.ZP_COL, 8
+    e.zpa, e.col, e.col_absmax = zpa, col.ptr, int(np.abs(col_h).max())
+    e.bias, e.b_packed, e.colterm = bias.ptr, kind, colterm.ptr
+    e.bt_pg = pg.ptr if use_pg else None
+    sa = 1.3e-4
+    if epi == EPI_QKV:
+        T, H, Dh = 197, N // 3 // 64, 64
+        e.group_cols, e.tokens, e.heads, e.hdim = N // 3, T, H, Dh
+        bufs = [DeviceArray((-(-M // T) * H * T, Dh), np.int8) for _ in range(3)]
+        for g in range(3):
+            e.s_acc[g] = float(np.float32(sa * (g + 1)))
+            e.s_out[g] = (0.0021, 0.0173, 0.05)[g] * s_out_scale
+            e.zp_out[g], e.out[g] = (3, -140, 0)[g], bufs[g].ptr
+    elif epi == EPI_RESID:
+        e.group_cols = 1 << 30
+        bufs = [DeviceArray((M, N), np.float32)]
+        e.s_acc[0], e.out[0], e.resid = float(np.float32(sa * 2)), bufs[0].ptr, resid.ptr
+    else:
+        e.group_cols = 1 << 30
+        bufs = [DeviceArray((M, N), np.int8)]
+        e.s_acc[0], e.s_out[0], e.zp_out[0], e.out[0] = float(np.float32(sa)), 0.0027 * s_out_scale, -9, bufs[0].ptr
+        e.div, e.add1, e.mul2 = float(np.float32(1.4142135381698608)), 1.0, 0.5
+    for b in bufs:
+        b.fill_zero()
+    _gemm(epi, a, packed, 1, M, N, K, K, K, None, 0, 0, e)
+    host = dict(a=a.to_host(), bt=bt_h, colterm=col_h * zpa, bias=bias.to_host(), resid=resid.to_host(), e=e)
+    return _last_kernel(), [b.to_host() for b in bufs], host
+
+
+def _numpy_ref(epi_name, M, N, K, host):
+    """The reference chain in NumPy (numpy_quantization.py:37-41 dequantize, model.py Add,
+    numpy_quantization.py:24-34 quantize) for small cases."""
+    e = host["e"]
+    acc = host["a"].astype(np.int64) @ host["bt"].astype(np.int64).T - host["colterm"][None, :]
+    if epi_name == "qkv":
+        T, H, Dh, G = e.tokens, e.heads, e.hdim, e.group_cols
+        outs = []
+        for g in range(3):
+            v = acc[:, g * G:(g + 1) * G]
+            d = (v.astype(np.float64) * np.float64(np.float32(e.s_acc[g]))).astype(np.float32)
+            y = d + host["bias"][g * G:(g + 1) * G]
+            t = y / np.float32(e.s_out[g])
+            q = np.rint(np.clip(np.float64(e.zp_out[g]) + t.astype(np.float64), -128, 127)).astype(np.int8)
+            nimg = -(-M // T)
+            o = np.zeros((nimg, H, T, Dh), np.int8)
+            qq = np.zeros((nimg * T, G), np.int8)
+            qq[:M] = q
+            o[:] = qq.reshape(nimg, T, H, Dh).transpose(0, 2, 1, 3)
+            outs.append(o.reshape(nimg * H * T, Dh))
+        return outs
+    return None
+
+
+@pytest.mark.parametrize("epi_name,M,N,K,s_out_scale,no_f32x", [
+    ("qkv", 256 * 197, 2304, 768, 1.0, False), ("qkv", 128 * 197, 2304, 768, 1.0, False),
+    ("qkv", 197, 2304, 768, 1.0, False), ("qkv", 512, 2304, 768, 0.05, False),
+    ("gelu", 128 * 50, 3072, 768, 1.0, False), ("gelu", 128 * 197, 3072, 768, 1.0, False),
+    ("gelu", 300, 3072, 768, 0.1, False),
+    ("resid", 128 * 200, 768, 768, 1.0, False), ("resid", 128 * 200, 768, 3072, 1.0, False),
+    ("resid", 128 * 197, 768, 3072, 1.0, True), ("resid", 300, 768, 768, 1.0, False),
+    ("resid", 256 * 197, 768, 3072, 1.0, False),
+])
+def test_pg_gemm_equals_big_tile(epi_name, M, N, K, s_out_scale, no_f32x, monkeypatch):
+    seed = M + N + K
+    k0, ref, host = _run(epi_name, M, N, K, s_out_scale, False, no_f32x, monkeypatch, seed)
+    k1, got, _ = _run(epi_name, M, N, K, s_out_scale, True, no_f32x, monkeypatch, seed)
+    assert (k0, k1) == (1, 4), (k0, k1)
+    if M <= 1024:
+        npref = _numpy_ref(epi_name, M, N, K, host)
+        if npref is not None:
+            bad_old = [int((x != r).sum()) for x, r in zip(ref, npref)]
+            bad_new = [int((y != r).sum()) for y, r in zip(got, npref)]
+            assert bad_old == [0] * len(npref) and bad_new == [0] * len(npref), (bad_old, bad_new)
+    for x, y in zip(ref, got):
+        np.testing.assert_array_equal(x, y)

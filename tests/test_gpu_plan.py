@@ -182,3 +182,38 @@ def test_vit_tiny_fused_plan_matches_node_loop_and_oracle():
     out = qmodel([x])[0]
     np.testing.assert_array_equal(out, eager)
     np.testing.assert_array_equal(out[:1], ref)
+
+
+def test_fused_run_leaves_no_stale_intermediates():
+    """after an eager keep_values run, a fused run with other inputs must not
+    leave the eager run's tensors in the values its steps compute internally: every value
+    either holds this run's tensor or raises on access (plan.FusedAway)."""
+    from numpy_quant.plan import FusedAway
+    rng = np.random.default_rng(7)
+    x1 = rng.standard_normal((2, 3, 224, 224)).astype(np.float32)
+    x2 = rng.standard_normal((2, 3, 224, 224)).astype(np.float32)
+    model = _vit(2)
+    qmodel = model.quantize([x1], bit_width=8)
+    qmodel.keep_values = True
+    qmodel([x1])
+    before = {id(v): v.data for v in qmodel.values}
+    qmodel.keep_values = False
+    qmodel.compile()
+    out2 = qmodel([x2])[0]
+    stale = []
+    for v in qmodel.values:
+        ins = getattr(v, "inputs", None)
+        if not ins or ins[0].op == "Constant":  # Constant values / Constant-node outputs persist
+            continue
+        if v in qmodel.inputs:
+            continue
+        if v.data is before[id(v)] and v.data is not None:
+            stale.append(v.name)
+    assert not stale, stale[:10]
+    n_away = sum(isinstance(v.data, FusedAway) for v in qmodel.values)
+    assert n_away > 100
+    with pytest.raises(RuntimeError):
+        next(v for v in qmodel.values if isinstance(v.data, FusedAway)).data.data
+    # and an eager run of x2 gives the same output
+    qmodel.keep_values = True
+    np.testing.assert_array_equal(qmodel([x2])[0], out2)
