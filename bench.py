@@ -23,11 +23,11 @@ rank processes itself from this parent, which never touches the GPU.  Rank 0
 calibrates; its QModel (every quantized constant + every quantization parameter,
 blob.py) reaches the other ranks as ONE RCCL broadcast over xGMI; each step every
 rank runs its own batch and the logits are gathered to rank 0 over RCCL.
-torch.distributed (gloo, CPU) is only the control plane.
+numpy_quant/control.py (a TCP star, no PyTorch) is only the control plane.
 
-After the timed loop each rank checks its own output: images at both ends of the two
-half-batch streams (0, B/2-1, B/2, B-1) must equal a batch-1 run of the same image
-through the reference's node-by-node loop, bit for bit ("verified" in the JSON).
+After the timed loop each rank checks its own output: all B rows must equal one batch-B
+run of the reference's node-by-node loop (QModel with keep_values), bit for bit
+("verified" in the JSON).
 """
 from __future__ import annotations
 

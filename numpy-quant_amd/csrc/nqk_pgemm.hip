@@ -36,6 +36,7 @@ namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -161,6 +162,25 @@ __device__ __forceinline__ int pg_quant_exact(float x, float s, double rs, doubl
   const float t = (float)((double)x * rs);  // RN32(x / s) (s normal, host-checked)
   const double u = zp + (double)t;
   return (int)__builtin_rint(__builtin_fmin(__builtin_fmax(u, lo), hi));
+}
+
+// gelu_fast (nqk_numerics.h) on two values with packed f32 arithmetic (v_pk_fma / v_pk_mul:
+// one instruction for both lanes of the pair, the same IEEE operations in the same order as
+// the scalar function, so the same bits: the epilogues are VALU-issue-bound and a packed
+// instruction issues at the scalar rate, tools/micro/valu.hip)
+__device__ __forceinline__ v2f gelu_fast2(v2f h) {
+  const v2f ah = __builtin_elementwise_abs(h);
+  const v2f d = __builtin_elementwise_fma(v2f{0.3275911f * 0.70710677f, 0.3275911f * 0.70710677f}, ah, v2f{1.0f, 1.0f});
+  const v2f t = v2f{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  v2f p = __builtin_elementwise_fma(v2f{0.5f * 1.061405429f, 0.5f * 1.061405429f}, t,
+                                    v2f{0.5f * -1.453152027f, 0.5f * -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, v2f{0.5f * 1.421413741f, 0.5f * 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, v2f{0.5f * -0.284496736f, 0.5f * -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, v2f{0.5f * 0.254829592f, 0.5f * 0.254829592f});
+  const v2f ea = h * (h * v2f{-0.72134752f, -0.72134752f});
+  const v2f ex = v2f{__builtin_amdgcn_exp2f(ea[0]), __builtin_amdgcn_exp2f(ea[1])};
+  const v2f q = (p * t) * ex;
+  return __builtin_elementwise_fma(-ah, q, __builtin_elementwise_max(h, v2f{0.0f, 0.0f}));
 }
 
 // Q_LIM = (0.5 - 2^-126)(1 - 2^-23) rounded down: a rounded fma measure below it keeps the
@@ -332,8 +352,36 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         uint32_t pk[4] = {0, 0, 0, 0};
         uint32_t worst = 0;
         float hv[16];
+        // the fast paths on element pairs (packed f32 arithmetic where an instruction exists)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
+        for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) == 0; q += 2) {
+          const v2f vf = v2f{(float)acc[i][q >> 2][q & 3], (float)acc[i][q >> 2][(q & 3) + 1]};
+          v2f rr;
+          float m0, m1;
+          if constexpr (EPI == PG_QKV) {
+            const v2f u = __builtin_elementwise_fma(vf, v2f{c1, c1}, v2f{c2[q], c2[q + 1]});
+            rr = v2f{__builtin_rintf(u[0]), __builtin_rintf(u[1])};
+            const v2f dd = u - rr;
+            m0 = __builtin_fmaf(__builtin_fabsf(vf[0]), k1, __builtin_fabsf(dd[0]));
+            m1 = __builtin_fmaf(__builtin_fabsf(vf[1]), k1, __builtin_fabsf(dd[1]));
+          } else {  // GELU: h exactly as the reference (F32X), then the filtered fast chain
+            const v2f h = v2f{bias[q], bias[q + 1]} + vf * v2f{sacc, sacc};
+            hv[q] = h[0];
+            hv[q + 1] = h[1];
+            const v2f tf = gelu_fast2(h) * v2f{rsf, rsf};
+            rr = v2f{__builtin_rintf(tf[0]), __builtin_rintf(tf[1])};
+            const v2f dd = tf - rr;
+            m0 = __builtin_fmaf(__builtin_fabsf(h[0]), e.g_rel, __builtin_fabsf(dd[0]));
+            m1 = __builtin_fmaf(__builtin_fabsf(h[1]), e.g_rel, __builtin_fabsf(dd[1]));
+          }
+          worst = __builtin_elementwise_max(worst, __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
+          const v2f b = rr + v2f{zp128, zp128};
+          pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[0], e.lo128, e.hi128), q & 3, pk[q >> 2]);
+          pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[1], e.lo128, e.hi128), (q & 3) + 1,
+                                                      pk[q >> 2]);
+        }
+#pragma unroll
+        for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) != 0; ++q) {
           const int a = acc[i][q >> 2][q & 3];
           const float vf = (float)a;
           float u;
@@ -399,48 +447,61 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     }
   };
 
-  // RESID epilogue: y = (bias + RN(v sacc)) + residual, f32 stores.  The residual rows of
-  // subtile i are loaded by 4 untracked 16-B loads (res_issue); subtiles 0 and 1 are issued
-  // before the next tile's stages (so waiting for them does not wait for the stages)
+  // RESID epilogue: y = (bias + RN(v sacc)) + residual, f32 stores, with whole 128-B lines
+  // per instruction: each subtile's accumulators go through the wave's part of ring slot 2
+  // (free from the barrier after the k loop until the next tile's step 0 refills it), row-
+  // major [16 rows][64 columns] int32 with 272-B rows, and come back transposed: lane
+  // (a = l & 15, b = l >> 4) takes row 4 k + b, columns 4 a .. 4 a + 3 for k = 0..3, so the
+  // 16 lanes of a row load / store its 256 contiguous bytes.  Residual loads of subtile i + 2
+  // are issued after subtile i's stores (0 and 1 before the next tile's stages); the
+  // compiler places their waits (compiler-visible loads).
   const rsrc_t r_res = pg_rsrc(RESID ? e.resid : nullptr, RESID ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
+  constexpr int TR_ROW = 272;  // bytes per staged row (256 + 16: conflict-free b128 writes)
+  int8_t* const tr = lds + 2 * PG_STG + wave * (16 * TR_ROW);
+  const int ta = lane & 15, tb = lane >> 4;
   v4u resv[3][4];
+  auto res_off = [&](const Src& s, int i, int k) __attribute__((always_inline)) {
+    return (uint32_t)(((s.r0 + 16 * i + 4 * k + tb) * e.ldo + s.tn * PG_BN + 64 * wave + 4 * ta) * 4);
+  };
   auto res_issue = [&](const Src& s, auto I) __attribute__((always_inline)) {
     constexpr int i = decltype(I)::value;
-    const uint32_t o = (uint32_t)(((s.r0 + 16 * i + l15) * e.ldo + s.tn * PG_BN + 64 * wave + 4 * lg) * 4);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) resv[i % 3][g] = pg_load16(r_res, o + 64 * g, 0u);
+    for (int k = 0; k < 4; ++k) resv[i % 3][k] = pg_load16(r_res, res_off(s, i, k), 0u);
   };
   auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
     const int8_t* cp = lds + PG_COLP + cslot * 2048;
-    float bias[16];
-    {
-      v4i bb[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) bb[g] = pg_lds16(cp + 1024 + (64 * wave + 16 * g + 4 * lg) * 4);
-      pg_lgkm_tie(bb[0], bb[1], bb[2], bb[3]);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) bias[q] = __int_as_float(bb[q >> 2][q & 3]);
-    }
+    const v4i bb = pg_lds16(cp + 1024 + (64 * wave + 4 * ta) * 4);  // columns 4 a .. 4 a + 3
+    const v2f b01 = v2f{__int_as_float(bb[0]), __int_as_float(bb[1])};
+    const v2f b23 = v2f{__int_as_float(bb[2]), __int_as_float(bb[3])};
     const rsrc_t r_out = pg_rsrc(e.out[0], (uint32_t)((uint64_t)M * e.ldo * 4));
     const float sacc = e.sacc[0];
     sfor<0, 8>([&](auto I) __attribute__((always_inline)) {
       constexpr int i = decltype(I)::value;
-      // (the compiler waits for subtile i's residual: its loads are visible to it)
+      // this lane's 16 accumulators: row l15, columns 16 j + 4 lg + r (layout 1)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<v4i*>(tr + l15 * TR_ROW + (16 * j + 4 * lg) * 4) = acc[i][j];
+      v4i t[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] = *reinterpret_cast<const v4i*>(tr + (4 * k + tb) * TR_ROW + 16 * ta);
       const v4u(&rv)[4] = resv[i % 3];
-      const uint32_t o = (uint32_t)(((s.r0 + 16 * i + l15) * e.ldo + s.tn * PG_BN + 64 * wave + 4 * lg) * 4);
-      float y[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int a = acc[i][q >> 2][q & 3];
-        const float d = F32X ? (float)a * sacc : (float)((double)a * (double)sacc);
-        y[q] = (bias[q] + d) + __uint_as_float(rv[q >> 2][q & 3]);
-      }
+      for (int k = 0; k < 4; ++k) {
+        v4u st;
+        if constexpr (F32X) {
+          const v2f d01 = v2f{(float)t[k][0], (float)t[k][1]} * v2f{sacc, sacc};
+          const v2f d23 = v2f{(float)t[k][2], (float)t[k][3]} * v2f{sacc, sacc};
+          const v2f y01 = (b01 + d01) + v2f{__uint_as_float(rv[k][0]), __uint_as_float(rv[k][1])};
+          const v2f y23 = (b23 + d23) + v2f{__uint_as_float(rv[k][2]), __uint_as_float(rv[k][3])};
+          st = v4u{__float_as_uint(y01[0]), __float_as_uint(y01[1]), __float_as_uint(y23[0]), __float_as_uint(y23[1])};
+        } else {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const v4u st = v4u{__float_as_uint(y[4 * g]), __float_as_uint(y[4 * g + 1]), __float_as_uint(y[4 * g + 2]),
-                           __float_as_uint(y[4 * g + 3])};
+          for (int r = 0; r < 4; ++r) {
+            const float d = (float)((double)t[k][r] * (double)sacc);
+            st[r] = __float_as_uint((__int_as_float(bb[r]) + d) + __uint_as_float(rv[k][r]));
+          }
+        }
         if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, o + 64 * g, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, res_off(s, i, k), 0, 0);
       }
       if constexpr (i + 2 < 8) res_issue(s, ic<i + 2>{});
     });
@@ -515,10 +576,12 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       });
     });
     // RESID: the residual rows of the first two subtiles, then the next tile's first
-    // stages (slots 0 and 1: last read before step NK - 2's barrier)
+    // stages (slots 0 and 1: last read before step NK - 2's barrier); a barrier frees slot 2
+    // (stage NK - 1) for the epilogue's transposes
     if constexpr (RESID) {
       res_issue(cur, ic<0>{});
       res_issue(cur, ic<1>{});
+      __builtin_amdgcn_s_barrier();
     }
     // (the last tile re-stages its own first stages: never read, drained at the end; the
     // VMEM counts stay the same on every path)

@@ -11,9 +11,12 @@ shared is set up once:
   source of truth and no other rank calibrates;
 * per step, each rank's logits are gathered into rank 0's HBM over RCCL.
 
-The control plane is torch.distributed with the gloo backend (CPU): rendezvous,
-the RCCL unique id, barriers and the max-over-ranks of the step time.  The device
-collectives are libnqk's `nqk_comm_*` (RCCL), never torch tensors.
+The control plane is control.py's TCP star (no PyTorch): rendezvous, the RCCL
+unique id, the blob header, barriers and the max-over-ranks of the step time.  The
+device collectives are libnqk's `nqk_comm_*` (RCCL).  With `force_device_comm`
+(NQK_FORCE_COMM=1) a single process also builds a 1-rank RCCL communicator and runs the
+broadcast / gather through it, so the device path runs on a 1-GPU box
+(tests/test_gpu_rccl.py).
 """
 from __future__ import annotations
 
@@ -30,38 +33,36 @@ def check_gather_sizes(rank: int, world: int, src_bytes: int, dst_bytes) -> None
 
 
 class ReplicaGroup:
-    def __init__(self, rank: int | None = None, world: int | None = None, init_process_group: bool = True):
+    def __init__(self, rank: int | None = None, world: int | None = None, force_device_comm: bool | None = None):
+        from .control import ControlPlane
         self.rank = int(os.environ.get("RANK", "0")) if rank is None else rank
         self.world = int(os.environ.get("WORLD_SIZE", "1")) if world is None else world
         self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
-        self.dist = None
+        if force_device_comm is None:
+            force_device_comm = os.environ.get("NQK_FORCE_COMM", "0") == "1"
+        self.force = bool(force_device_comm)
         self.device_comm = False
-        if self.world > 1:
-            import torch.distributed as dist
-            if init_process_group and not dist.is_initialized():
-                dist.init_process_group("gloo", init_method="env://")
-            self.dist = dist
+        self.ctrl = ControlPlane(self.rank, self.world)
+
+    @property
+    def use_device_comm(self) -> bool:
+        return self.world > 1 or self.force
 
     # ------------------------------------------------------------------ control plane
     def broadcast_object(self, obj, src: int = 0):
+        """A JSON-able object (or bytes) of rank `src` on every rank."""
+        from .control import decode_bytes, encode_bytes
         if self.world == 1:
             return obj
-        box = [obj if self.rank == src else None]
-        self.dist.broadcast_object_list(box, src=src)
-        return box[0]
+        out = self.ctrl.broadcast(encode_bytes(obj) if isinstance(obj, bytes) else obj, src=src)
+        return decode_bytes(out) if isinstance(out, dict) and "__bytes__" in out else out
 
     def barrier(self) -> None:
-        if self.world > 1:
-            self.dist.barrier()
+        self.ctrl.barrier()
 
     def max(self, x: float) -> float:
         """Max over ranks (the bench's step time)."""
-        if self.world == 1:
-            return float(x)
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t[0])
+        return self.ctrl.allreduce_max(x)
 
     def shared_calibration(self, calibrate):
         """Run `calibrate()` -> (vmin, vmax) on rank 0 only and hand every rank the
@@ -78,7 +79,7 @@ class ReplicaGroup:
 
     # ------------------------------------------------------------------ device (RCCL)
     def init_device_comm(self) -> None:
-        if self.world == 1 or self.device_comm:
+        if not self.use_device_comm or self.device_comm:
             return
         from . import _lib
         uid = (ctypes.c_char * 128)()
@@ -92,8 +93,10 @@ class ReplicaGroup:
     def broadcast_qmodel(self, model, qmodel=None):
         """Rank 0 passes its QModel; every rank returns (qmodel, payload bytes): rank 0
         its own, the others one built on `model`'s graph from rank 0's blob, received
-        with a single ncclBroadcast of the packed payload."""
-        if self.world == 1:
+        with a single ncclBroadcast of the packed payload.  Forced device comm at world 1:
+        the packed blob goes through a 1-rank ncclBroadcast and the returned QModel is the
+        one attached to it (the device path of the other ranks, run on one GPU)."""
+        if not self.use_device_comm:
             return qmodel, 0
         from . import _lib, blob
         from .device import DeviceArray
@@ -110,7 +113,7 @@ class ReplicaGroup:
         if n:
             _lib.call("nqk_comm_bcast", payload.vp, n, 0)
         _lib.call("nqk_sync")
-        if self.rank == 0:
+        if self.rank == 0 and self.world > 1:
             return qmodel, n
         return blob.attach(model, header, payload), n
 
@@ -118,7 +121,7 @@ class ReplicaGroup:
         """Broadcast every device-resident constant of `qmodel` from rank 0, one
         collective per constant (kept for models built on every rank; bench.py uses
         broadcast_qmodel's single blob broadcast)."""
-        if self.world == 1:
+        if not self.use_device_comm:
             return 0
         from . import _lib
         self.init_device_comm()
@@ -133,10 +136,11 @@ class ReplicaGroup:
 
     def gather(self, src, dst=None) -> None:
         """Gather each rank's `src` DeviceArray into rank 0's `dst` [world, *src.shape]."""
-        if self.world == 1:
+        if not self.use_device_comm or (self.world == 1 and dst is None):
             return
         from . import _lib
         check_gather_sizes(self.rank, self.world, src.nbytes, None if dst is None else dst.nbytes)
+        self.init_device_comm()
         _lib.call("nqk_comm_gather", src.vp, dst.vp if self.rank == 0 else None, src.nbytes, 0)
 
     def close(self) -> None:
@@ -144,5 +148,4 @@ class ReplicaGroup:
             from . import _lib
             _lib.call("nqk_comm_destroy")
             self.device_comm = False
-        if self.dist is not None and self.dist.is_initialized():
-            self.dist.destroy_process_group()
+        self.ctrl.close()

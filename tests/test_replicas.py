@@ -1,4 +1,4 @@
-"""Multi-process replicas on the CPU: world_size 2 over gloo.
+"""Multi-process replicas on the CPU: world_size 2 over the TCP control plane.
 
 Covers the control plane of bench.py's N > 1 path — rank-0 calibration shared with
 every replica (bit-identical quantization parameters on all ranks), the RCCL
@@ -10,7 +10,7 @@ import socket
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+import multiprocessing as mp
 
 from numpy_quant.numpy_quantization import quant_parameters
 from numpy_quant.replicas import ReplicaGroup
