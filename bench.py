@@ -406,6 +406,7 @@ def main(argv=None):
     ap.add_argument("--bit-width", type=int, default=8)
     ap.add_argument("--config", choices=("vit", "vit_int4", "vit_tiny", "mlp4096"), default="vit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the int4 / ViT-tiny / MLP-4096 lines")
     ap.add_argument("--graph", type=int, default=0, help="1: replay the ViT forward as one captured hipGraph")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # launcher test: no GPU
     args = ap.parse_args(argv)
@@ -437,10 +438,36 @@ def main(argv=None):
     _lib.ensure_init(group.local_rank)
     try:
         res = run_mlp(args, group) if args.config == "mlp4096" else run_vit(args, group)
+        if res is not None and args.config == "vit" and world == 1 and not args.no_secondary:
+            res["secondary"] = run_secondary(args, group)
         if res is not None:
             print(json.dumps(res), flush=True)
     finally:
         group.close()
+
+
+def run_secondary(args, group) -> dict:
+    """The other BASELINE.json configs, measured in the same process after the headline
+    line (not part of `value`): configs[4] ViT-Base int4 nibble-packed weights, the metric's
+    ViT-tiny (the graph re-dimensioned), configs[1] mlp.onnx at batch 4096.  Each with
+    its own whole-batch parity check."""
+    import copy
+    out = {}
+    for cfg in ("vit_int4", "vit_tiny", "mlp4096"):
+        sub = copy.copy(args)
+        sub.config, sub.steps, sub.warmup, sub.no_cpu_baseline = cfg, min(args.steps, 10), min(args.warmup, 2), True
+        sub.graph = 0
+        t0 = time.time()
+        try:
+            r = run_mlp(sub, group) if cfg == "mlp4096" else run_vit(sub, group)
+            keep = ("value", "unit", "ms_per_step", "steps", "dtype", "verified", "checked_images", "config")
+            out[cfg] = {k: r[k] for k in keep if k in r}
+            if "roofline" in r:
+                out[cfg]["roofline_frac"] = r["roofline"]["frac"]
+        except Exception as e:  # a failing secondary must not lose the headline line
+            out[cfg] = {"error": repr(e)[:300]}
+        log(f"[bench] secondary {cfg}: {out[cfg].get('value')} samples/s in {time.time() - t0:.1f}s")
+    return out
 
 
 if __name__ == "__main__":

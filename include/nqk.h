@@ -260,7 +260,8 @@ int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, i
 /* Which kernel the last nqk_qgemm_fused call launched (tests / diagnostics): 0 small tiles
  * (k_qgemm_epi), 1 128x256 tiles (k_qgemm_big), 2 ping-pong 256x256 (k_qgemm_pp), 3 the
  * persistent projection GEMM with the epilogue overlapped (k_proj), 4 the persistent 16x16x64
- * GEMM with two workgroups per CU (k_pg); -1 none yet. */
+ * GEMM with two workgroups per CU (k_pg), 5 the persistent 16x16x64 GEMM with each tile's
+ * epilogue inside the next tile's k loop (k_pg2); -1 none yet. */
 int nqk_qgemm_last_kernel(void);
 /* LayerNormalization (model.py:134-152) fused with the consumer MatMul's quantize */
 int nqk_ln_quant(const float* x, const float* gamma, const float* beta, int8_t* out, int64_t rows, int64_t cols,
@@ -293,8 +294,9 @@ int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_t* v, int8_
 /* Diagnostic: on the device, compares the fast-division variants of NumPy's exp and the
  * reference's erf (used by the fused kernels) with the IEEE-division ones on all 2^32
  * float inputs; adds the mismatch counts to counts_dev[0] (exp) / [1] (erf), and those of
- * the attention kernel's non-positive-argument exp against NumPy's exp to [2] (all 2^31
- * inputs x <= 0).  counts_dev and examples_dev hold 3 entries each. */
+ * the attention kernel's non-positive-argument exp against NumPy's exp to [2] and of its
+ * packed two-lane variant to [3] (all 2^31 inputs x <= 0).  counts_dev and examples_dev
+ * hold 4 entries each. */
 int nqk_selftest_fastmath(unsigned long long* counts_dev, uint32_t* examples_dev);
 /* Diagnostic: checks the error bound of the GELU filter's cheap approximation on all
  * 2^32 inputs; stats_dev[0] = violations, [1] = an example, [2 + e] = max error per

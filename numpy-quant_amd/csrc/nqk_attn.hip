@@ -13,7 +13,9 @@
 //
 // LDS (T = 197: NT = 7 score tiles of 32 columns):
 //   Ks   [NT*32][64]     int8, 16-byte chunks XOR-swizzled (conflict-free A reads)
-//   Vt   [64][PST]       int8 V^T, zero padded to NT*32 tokens; PST = NT*32 + 16
+//   Vt   [64][PST]       int8 V^T, zero padded to NT*32 tokens; PST = NT*32 + 16, and dims
+//                        16c .. 16c + 15 shifted by 64 c bytes (vt_row): conflict-free dword
+//                        writes of the transposed staging
 //   colK [NT*32], colV [64]   int32 zero-point column terms
 // 30 KiB per workgroup: three workgroups (12 waves) per CU; everything else is in VGPRs.
 #include "nqk_common.h"
@@ -24,6 +26,9 @@
 #endif
 #ifndef NQK_ATTN_EXPW
 #define NQK_ATTN_EXPW 4
+#endif
+#ifndef NQK_ATTN_PK
+#define NQK_ATTN_PK 1  // FAST path on element pairs with packed f32 arithmetic (0: scalar, for A/B)
 #endif
 
 namespace nqk {
@@ -122,7 +127,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   const int T = TC ? TC : a.T, PST = TC ? NT * 32 + 16 : a.PST;
   int8_t* Ks = lds;
   int8_t* Vt = Ks + TP * 64;
-  int* colK = reinterpret_cast<int*>(Vt + 64 * PST);  // rowsum(K[n]) * zq - zq*zk*64
+  auto vt_row = [&](int d) { return d * PST + (d >> 4) * 64; };  // byte offset of V^T row d
+  int* colK = reinterpret_cast<int*>(Vt + 64 * PST + 256);  // rowsum(K[n]) * zq - zq*zk*64
   int* colV = colK + TP;                              // colsum(V[:, d]) * zp - zp*zv*T
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x;
@@ -136,16 +142,35 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     const int row = idx >> 2, ch = idx & 3;
     const v4i z = {0, 0, 0, 0};
     const v4i kv = row < T ? *reinterpret_cast<const v4i*>(k + row * 64 + ch * 16) : z;
-    const v4i vv = row < T ? *reinterpret_cast<const v4i*>(v + row * 64 + ch * 16) : z;
     *reinterpret_cast<v4i*>(Ks + swz64a(row, ch)) = kv;
+  }
+  // V^T by blocks of 4 tokens x 16 dims: four 16-B row loads, a 4 x 4 byte transpose per
+  // dword column (v_perm_b32), sixteen 4-byte writes of 4 consecutive tokens of one dim
+  // (consecutive lanes: consecutive token blocks of one 16-dim chunk)
+  for (int blk = tid; blk < TP; blk += 256) {  // TP / 4 token blocks x 4 dim chunks
+    const int c = blk / (TP / 4), rb = blk - c * (TP / 4);
+    v4i w[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tok = 4 * rb + r;
+      w[r] = tok < T ? *reinterpret_cast<const v4i*>(v + tok * 64 + c * 16) : v4i{0, 0, 0, 0};
+    }
 #if NQK_ATTN_DIAG & 1  // diagnostic builds only (wrong results): 1 = V^T staging skipped, 2 = exp
                       // replaced by one add, 4 = P quantize replaced by a convert
-    if (row == 0) Vt[ch] = (int8_t)vv[0];
+    if (blk == 0) Vt[0] = (int8_t)(w[0][0] ^ w[1][1] ^ w[2][2] ^ w[3][3]);
 #else
 #pragma unroll
-    for (int w = 0; w < 4; ++w)
+    for (int g = 0; g < 4; ++g) {
+      // out_k = [w0.byte k, w1.byte k, w2.byte k, w3.byte k] of dword column g
+      const uint32_t lo01 = __builtin_amdgcn_perm((uint32_t)w[1][g], (uint32_t)w[0][g], 0x05010400u);
+      const uint32_t hi01 = __builtin_amdgcn_perm((uint32_t)w[1][g], (uint32_t)w[0][g], 0x07030602u);
+      const uint32_t lo23 = __builtin_amdgcn_perm((uint32_t)w[3][g], (uint32_t)w[2][g], 0x05010400u);
+      const uint32_t hi23 = __builtin_amdgcn_perm((uint32_t)w[3][g], (uint32_t)w[2][g], 0x07030602u);
+      const uint32_t o[4] = {__builtin_amdgcn_perm(lo23, lo01, 0x05040100u), __builtin_amdgcn_perm(lo23, lo01, 0x07060302u),
+                             __builtin_amdgcn_perm(hi23, hi01, 0x05040100u), __builtin_amdgcn_perm(hi23, hi01, 0x07060302u)};
 #pragma unroll
-      for (int b = 0; b < 4; ++b) Vt[(ch * 16 + w * 4 + b) * PST + row] = (int8_t)(vv[w] >> (8 * b));
+      for (int kk = 0; kk < 4; ++kk) *reinterpret_cast<uint32_t*>(Vt + vt_row(16 * c + 4 * g + kk) + 4 * rb) = o[kk];
+    }
 #endif
   }
   __syncthreads();
@@ -156,7 +181,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   {
     const int d = tid >> 2, part = tid & 3;
     int s = 0;
-    for (int c = part; c < NT * 2; c += 4) s += sum16a(*reinterpret_cast<const v4i*>(Vt + d * PST + c * 16));
+    for (int c = part; c < NT * 2; c += 4) s += sum16a(*reinterpret_cast<const v4i*>(Vt + vt_row(d) + c * 16));
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     if (part == 0) colV[d] = s * a.zp - a.kp;
@@ -216,6 +241,22 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           for (int j = 0; j < 4; ++j) e[c][4 * qq + j] = 0.0f;
           continue;
         }
+        if constexpr (FAST && NQK_ATTN_PK) {
+          // pairs: one v_pk_mul for the dequantize + Div, a v_max3 for the row max; the
+          // -inf of padded columns only where the group straddles T (runtime lane half)
+          const bool full = TC > 0 && c * 32 + 8 * qq + 8 <= TC;
+#pragma unroll
+          for (int j = 0; j < 4; j += 2) {
+            const int r = 4 * qq + j, n = c * 32 + 8 * qq + 4 * h + j;
+            v2f_t y = v2f_t{(float)acc[r], (float)acc[r + 1]} * v2f_t{a.s_qkd, a.s_qkd};
+            if (!full) y = y + v2f_t{n < T ? 0.0f : -__builtin_inff(), n + 1 < T ? 0.0f : -__builtin_inff()};
+            e[c][r] = y[0];
+            e[c][r + 1] = y[1];
+            mx = __builtin_fmaxf(mx, __builtin_fmaxf(y[0], y[1]));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          continue;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * qq + j, n = c * 32 + 8 * qq + 4 * h + j;
@@ -237,6 +278,18 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
       mx = o > mx ? o : mx;
     }
     const float nm = -mx;
+    if constexpr (FAST && NQK_ATTN_PK && (NQK_ATTN_DIAG & 2) == 0) {
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          if (pad_group(c, r >> 2)) continue;  // stays 0
+          const v2f_t x = np_expf_nonpos2(v2f_t{e[c][r], e[c][r + 1]} + v2f_t{nm, nm});
+          e[c][r] = x[0];
+          e[c][r + 1] = x[1];
+          if ((r % NQK_ATTN_EXPW) == NQK_ATTN_EXPW - 2) __builtin_amdgcn_sched_barrier(0);
+        }
+    } else
 #pragma unroll
     for (int c = 0; c < NT; ++c)
 #pragma unroll
@@ -294,6 +347,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     // the filter's bound for the whole row (|tf| <= kpf (1 + 2^-23)), with margin
     const float plim = 0.5f - 2.0f * __builtin_fmaf(kpf, 0x1p-21f, 0x1p-126f);
     const float zp128 = a.zp_p_f + 128.0f, lo128 = a.lo_f + 128.0f, hi128 = a.hi_f + 128.0f;
+    const float pqlo = a.lo_f - a.zp_p_f, pqhi = a.hi_f - a.zp_p_f, pmagic = 0x1.8p23f + a.zp_p_f;
     // ---- per score tile c: P = quantize(e / tot) (4 packed bytes per group, row sums),
     // then at once its share of O^T = V^T P^T (B operand = P row m, 16 consecutive tokens
     // per half), so only one tile's packed P is live
@@ -320,6 +374,26 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         for (int qq = 0; qq < 4; ++qq) {
           if (pad_group(c, qq)) {
             dw[qq] = 0;
+            continue;
+          }
+          if constexpr (NQK_ATTN_PK) {
+            // pairs: one v_pk_mul for tf, the clamp / magic-number rounding + byte pack of
+            // round_magic2 / pack4_low (nqk_numerics.h), |dd| into the tile's worst
+            v2f_t dd0, dd1;
+            const v2f_t s0 = round_magic2(v2f_t{e[c][4 * qq], e[c][4 * qq + 1]} * v2f_t{kpf, kpf}, pqlo, pqhi, pmagic, dd0);
+            const v2f_t s1 =
+                round_magic2(v2f_t{e[c][4 * qq + 2], e[c][4 * qq + 3]} * v2f_t{kpf, kpf}, pqlo, pqhi, pmagic, dd1);
+            worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd0[0]), __builtin_fabsf(dd0[1])));
+            worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd1[0]), __builtin_fabsf(dd1[1])));
+            uint32_t w = pack4_low(s0, s1);
+            if (!(TC > 0 && c * 32 + 8 * qq + 8 <= TC)) {  // padded columns: 0
+              const int n = c * 32 + 8 * qq + 4 * h;
+              uint32_t keep = 0;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) keep |= (n + j < T ? 0xffu : 0u) << (8 * j);
+              w &= keep;
+            }
+            dw[qq] = (int)w;
             continue;
           }
           uint32_t packed = 0;
@@ -390,7 +464,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
       else   { pb[0] = dw[0]; pb[1] = xa; pb[2] = dw[1]; pb[3] = xb; }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const v4i va = *reinterpret_cast<const v4i*>(Vt + (j * 32 + r32) * PST + (2 * c + h) * 16);
+        const v4i va = *reinterpret_cast<const v4i*>(Vt + vt_row(j * 32 + r32) + (2 * c + h) * 16);
         acc2[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(va, pb, acc2[j], 0, 0, 0);
       }
     }
@@ -505,7 +579,7 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   const bool fast = bs < 16777216.0 && bp < 16777216.0 && dm == 0.5f && llabs(p->zp_ctx) < (1 << 20) &&
                     normal(a.s_qkd) && normal(p->s_qk) &&
                     !getenv("NQK_ATTN_EXACT");
-  const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + (size_t)(NT * 32 + 64) * 4;
+  const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + 256 + (size_t)(NT * 32 + 64) * 4;
   const dim3 grid((unsigned)batch_heads);
   switch (T == 197 ? (fast ? -1 : 0) : NT) {
 #define A(n) case n: hipLaunchKernelGGL((k_attention<n, 0, false>), grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;

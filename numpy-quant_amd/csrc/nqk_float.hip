@@ -250,10 +250,12 @@ __global__ void __launch_bounds__(256) k_minmax_final(const float* __restrict__ 
 }
 
 // exhaustive check: fast vs IEEE-division variants of np_expf / ref_erf on all 2^32
-// bit patterns; counts[0] / counts[1] = mismatching exp / erf inputs, ex[0..1] = an example
+// bit patterns; counts[0] / counts[1] = mismatching exp / erf inputs, counts[2] / counts[3]
+// = non-positive inputs where np_expf_nonpos / np_expf_nonpos2 (both lanes) differ from
+// np_expf; ex[k] = an example
 __global__ void k_fastmath_check(unsigned long long* counts, uint32_t* ex) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  unsigned long long ce = 0, cr = 0, cn = 0;
+  unsigned long long ce = 0, cr = 0, cn = 0, cp = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t(1) << 32); i += stride) {
     const float x = __uint_as_float((uint32_t)i);
     const float a = np_expf_t<true>(x), b = np_expf_t<false>(x);
@@ -261,10 +263,18 @@ __global__ void k_fastmath_check(unsigned long long* counts, uint32_t* ex) {
     const float c = ref_erf_t<true>(x), d = ref_erf_t<false>(x);
     if (__float_as_uint(c) != __float_as_uint(d) && !(c != c && d != d)) { ++cr; ex[1] = (uint32_t)i; }
     if (x <= 0.0f && __float_as_uint(np_expf_nonpos(x)) != __float_as_uint(b)) { ++cn; ex[2] = (uint32_t)i; }
+    if (x <= 0.0f) {
+      const v2f_t p = np_expf_nonpos2(v2f_t{x, x});
+      if (__float_as_uint(p[0]) != __float_as_uint(b) || __float_as_uint(p[1]) != __float_as_uint(b)) {
+        ++cp;
+        ex[3] = (uint32_t)i;
+      }
+    }
   }
   if (ce) atomicAdd(counts, ce);
   if (cr) atomicAdd(counts + 1, cr);
   if (cn) atomicAdd(counts + 2, cn);
+  if (cp) atomicAdd(counts + 3, cp);
 }
 
 // exhaustive check of the GELU filter bound (nqk_numerics.h gelu_fast) for the graph

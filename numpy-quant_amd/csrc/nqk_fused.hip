@@ -1877,10 +1877,10 @@ static Epi make_epi(const nqk_epilogue* p) {
     e.zpf[g] = (float)p->zp_out[g];
   }
   // GELU filter error in units of t: |gelu_fast - gelu| <= GELU_REL |h| + GELU_ABS, and
-  // the product t = y * rsf adds |t| 2^-22 <= |h| |1/s| 2^-21.9 (|gelu(h)| <= |h|), i.e.
-  // 0.27 GELU_REL |h| |1/s| at most; 2 % margin on 1/s
+  // the product t = y * rsf adds |t| 2^-22 <= |h| |1/s| 2^-21.9 (|gelu(h)| <= |h|;
+  // 0x1.13p-22 > 2^-21.9); 2 % margin on 1/s
   const double ars = __builtin_fabs(1.0 / (double)p->s_out[0]) * 1.02;
-  e.g_rel = (float)((double)GELU_REL * 1.27 * ars);
+  e.g_rel = (float)(((double)GELU_REL + 0x1.13p-22) * ars);
   e.g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
   // |tf - r| + |h| g_rel + g_abs < 0.5 tested as RN(|h| g_rel + |tf - r|) < g_lim: a
   // rounded-down sum below g_lim = (0.5 - g_abs)(1 - 2^-22) keeps the exact one below
@@ -1964,8 +1964,8 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
       const bool f32x_r = i32 && epi == EPI_RESID && 16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
       const int rc = pg_launch(epi, a, params->bt_pg, M, N, K, lda, params, f32x || f32x_r);
       if (rc < 0) return rc;
-      if (rc == 1) {
-        g_last_gemm = 4;
+      if (rc > 0) {
+        g_last_gemm = rc;
         return 0;
       }
     }

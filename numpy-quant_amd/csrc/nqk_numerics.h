@@ -78,6 +78,60 @@ __device__ __forceinline__ float np_expf_nonpos(float x) {
   return under ? 0.0f : poly;
 }
 
+// np_expf_nonpos on two values with packed f32 arithmetic (v_pk_fma / v_pk_mul: per lane
+// the same IEEE operations as the scalar code) for the softmax of the fused attention.
+// Instead of the underflow select, x is clamped to -128 first: NumPy's underflow region
+// x <= -103.97... has q <= -150 and, at q = -150, a remainder r <= 0 (so |poly| <= 1 and
+// poly 2^-150 rounds to 0), and every q <= -151 scales |poly| <= 2^0.5 below half the
+// smallest subnormal; the clamp also keeps -inf (padded score columns) out of the
+// reduction.  Equal to np_expf on all 2^31 non-positive inputs (nqk_selftest_fastmath,
+// counts[3]).
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2f_t np_expf_nonpos2(v2f_t x) {
+  const v2f_t xc = v2f_t{__builtin_fmaxf(x[0], -128.0f), __builtin_fmaxf(x[1], -128.0f)};
+  const float l2e = 1.442695040888963407359924681001892137f;
+  const v2f_t t = xc * v2f_t{l2e, l2e};
+  const v2f_t q = v2f_t{__builtin_rintf(t[0]), __builtin_rintf(t[1])};
+  v2f_t r = __builtin_elementwise_fma(q, v2f_t{-6.93145752e-1f, -6.93145752e-1f}, xc);
+  r = __builtin_elementwise_fma(q, v2f_t{-1.42860677e-6f, -1.42860677e-6f}, r);
+  auto c2 = [](float c) { return v2f_t{c, c}; };
+  v2f_t num = __builtin_elementwise_fma(c2(5.082762527590693718096e-04f), r, c2(6.757896990527504603057e-03f));
+  num = __builtin_elementwise_fma(num, r, c2(5.114512081637298353406e-02f));
+  num = __builtin_elementwise_fma(num, r, c2(2.473615434895520810817e-01f));
+  num = __builtin_elementwise_fma(num, r, c2(7.257664613233124478488e-01f));
+  num = __builtin_elementwise_fma(num, r, c2(9.999999999980870924916e-01f));
+  v2f_t den = __builtin_elementwise_fma(c2(2.159509375685829852307e-02f), r, c2(-2.742335390411667452936e-01f));
+  den = __builtin_elementwise_fma(den, r, c2(1.0f));
+  // div_t<true> on both lanes
+  const v2f_t rc = v2f_t{__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+  const v2f_t qq = num * rc;
+  const v2f_t e = __builtin_elementwise_fma(-den, qq, num);
+  const v2f_t res = __builtin_elementwise_fma(e, rc, qq);
+  return v2f_t{__builtin_ldexpf(res[0], (int)q[0]), __builtin_ldexpf(res[1], (int)q[1])};
+}
+
+// Round-and-pack of an element pair on the fast path.  c = clamp(x, lo - zp, hi - zp) (med3;
+// clamping before rounding is the same as after for integer bounds), s = RN(c + MAGIC) with
+// MAGIC = 1.5 2^23 + zp: s lies in [2^23, 2^24) where the f32 spacing is 1, so s = rint(c) +
+// MAGIC exactly and the low mantissa byte of s is the two's complement byte of rint(c) + zp.
+// (At an exact tie an odd zp flips the even choice, but then |dd| = 0.5 fails every filter
+// limit and the element takes the exact chain.)
+// dd = c - (s - MAGIC) is the filter's distance to the rounded value (exact).  Replaces
+// v_rndne + add zp + med3 + v_cvt_pk_u8 + xor 0x80 per element (nqk_fused.hip
+// quant_filter); used by the GELU GEMM and the attention epilogues.
+__device__ __forceinline__ v2f_t round_magic2(v2f_t x, float qlo, float qhi, float magic, v2f_t& dd) {
+  const v2f_t c = v2f_t{__builtin_amdgcn_fmed3f(x[0], qlo, qhi), __builtin_amdgcn_fmed3f(x[1], qlo, qhi)};
+  const v2f_t s = c + v2f_t{magic, magic};
+  dd = c - (s - v2f_t{magic, magic});
+  return s;
+}
+// the low bytes of four rounded values (round_magic2) as one dword
+__device__ __forceinline__ uint32_t pack4_low(v2f_t s01, v2f_t s23) {
+  const uint32_t x = __builtin_amdgcn_perm(__float_as_uint(s01[1]), __float_as_uint(s01[0]), 0x0c0c0400u);
+  const uint32_t y = __builtin_amdgcn_perm(__float_as_uint(s23[1]), __float_as_uint(s23[0]), 0x04000c0cu);
+  return x | y;
+}
+
 // numpy_helper.py:95-112 (A&S 7.1.26), float32 throughout
 template <bool FAST>
 __device__ __forceinline__ float ref_erf_t(float x) {
@@ -107,7 +161,8 @@ __device__ __forceinline__ float gelu_ref(float h, double rdiv, float add1, floa
 // checks on the GPU, for every one of the 2^32 f32 inputs with |h| < 2^64, that
 // |gelu_fast(h) - gelu_ref(h)| <= GELU_REL * |h| + GELU_ABS; the GEMM epilogue only
 // trusts gelu_fast where that bound cannot move the quantized value (nqk_fused.hip).
-constexpr float GELU_REL = 0x1p-20f, GELU_ABS = 0x1p-60f;
+// (measured worst case: 7 |h| 2^-24 at exponents -10..-3, tests/test_gpu_kernels.py)
+constexpr float GELU_REL = 0x1p-21f, GELU_ABS = 0x1p-60f;
 // With A&S 7.1.26 erf(x) = 1 - P(t) t e^{-x^2}, t = 1 / (1 + p|x|), x = h / sqrt2, the
 // GELU h (1 + erf(x)) / 2 is max(h, 0) - |h| q with q = P(t) t e^{-h^2/2} / 2 (the 1/2
 // and 1/sqrt2 folded into the constants): 11 VALU + v_rcp + v_exp.

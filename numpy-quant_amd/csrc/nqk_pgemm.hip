@@ -32,6 +32,16 @@
 #include "nqk_numerics.h"
 
 namespace nqk {
+#if (NQK_PG_DIAG & 64)
+__device__ unsigned long long g_pg_slow[2];
+extern "C" unsigned long long nqk_pg_diag_slow(int reset) {
+  unsigned long long v[2] = {0, 0};
+  (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_pg_slow), sizeof(v));
+  const unsigned long long z[2] = {0, 0};
+  if (reset) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pg_slow), z, sizeof(z));
+  return v[0];
+}
+#endif
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -96,7 +106,7 @@ __device__ __forceinline__ v4i pg_lds16(const void* p) {
 #endif
 template <int OFF>
 __device__ __forceinline__ v4i pg_lds16o(const int8_t* base) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds_read offset");
+  static_assert(OFF >= 0 && (OFF < 65536 || !NQK_PG_ASMREAD), "ds_read offset");
   if constexpr (NQK_PG_ASMREAD) {
     v4i v;
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)base), "n"(OFF));
@@ -140,14 +150,14 @@ struct PgEpi {
   float rsf[3];       // RN32(1 / s_out)
   float c1[3];        // RN32(sacc * rsf)            (QKV fast path)
   float k1[3];        // |c1| 2^-21                  (QKV filter: rounding error per |v|)
-  float zp128[3];     // zp_out + 128 (f32)
+  float zp128[3];     // zp_out + 128 (f32)        (QKV: v_rndne + v_cvt_pk_u8 rounding)
+  float qlo[3], qhi[3], magic[3];  // lo - zp, hi - zp, 1.5 2^23 + zp (GELU: pg_round2)
   float s_out[3];
   double rs_out[3], zp_out[3];
   void* out[3];
   const float* bias;
   const float* resid;
   const int32_t* colterm;  // col[n] * zpa (int32)
-  float lo128, hi128;
   double lo, hi;
   int group_cols, tokens, heads, hdim;
   float g_rel, g_lim;  // GELU filter (nqk_fused.hip make_epi)
@@ -162,6 +172,61 @@ __device__ __forceinline__ int pg_quant_exact(float x, float s, double rs, doubl
   const float t = (float)((double)x * rs);  // RN32(x / s) (s normal, host-checked)
   const double u = zp + (double)t;
   return (int)__builtin_rint(__builtin_fmin(__builtin_fmax(u, lo), hi));
+}
+
+// per-column-group constants of the exact fallback
+struct PgFix {
+  float c1, k1, rsf, sacc, lim, s_out;
+  double rs_out, zp;
+};
+// The rounding filter's exact fallback for element q of one epilogue step: recheck the
+// element's filter measure, and run the reference chain where it could not decide.
+// av: the int32 accumulators; xv: QKV the column bias, GELU h = RN(bias + RN(v sacc)).
+template <int EPI>
+__device__ __forceinline__ void pg_exact_fix1(int q, const int (&av)[16], const float (&xv)[16], uint32_t (&pk)[4],
+                                              const PgFix& f, const PgEpi& e) {
+  const float vf = (float)av[q];
+  const float x = xv[q];
+  bool slow;
+  if constexpr (EPI == PG_QKV) {
+    const float u = __builtin_fmaf(vf, f.c1, x * f.rsf);
+    const float r = __builtin_rintf(u);
+    slow = !(__builtin_fmaf(__builtin_fabsf(vf), f.k1, __builtin_fabsf(u - r)) < f.lim);
+  } else {
+    const float tf = gelu_fast(x) * f.rsf;
+    const float r = __builtin_rintf(tf);
+    slow = !(__builtin_fmaf(__builtin_fabsf(x), e.g_rel, __builtin_fabsf(tf - r)) < f.lim);
+  }
+  if (__any(slow)) {
+    if (slow) {
+      float y;
+      if constexpr (EPI == PG_QKV) {
+        y = x + vf * f.sacc;  // F32X: the f64 dequantize, exactly
+      } else {
+        y = x;
+        const float aa = ref_erf((float)((double)y * e.rdiv)) + e.add1;
+        y = (y * aa) * e.mul2;
+      }
+      const int qv = pg_quant_exact(y, f.s_out, f.rs_out, f.zp, e.lo, e.hi);
+      const int sh = 8 * (q & 3);
+      pk[q >> 2] = (pk[q >> 2] & ~(0xffu << sh)) | ((uint32_t)(qv & 0xff) << sh);
+    }
+  }
+}
+// ... for all 16 elements of the step (entered when any lane's worst measure fails).  GELU:
+// a loop that is not unrolled (av / xv / pk indexed by the wave-uniform q stay in VGPRs via
+// relative moves), so the long exact chain is not duplicated per element and per step; QKV:
+// unrolled (its exact chain is short; measured faster, profiles/r03_pg_micro.txt).
+template <int EPI>
+__device__ __forceinline__ void pg_exact_fix(const int (&av)[16], const float (&xv)[16], uint32_t (&pk)[4],
+                                             const PgFix& f, const PgEpi& e) {
+  if constexpr (EPI == PG_QKV) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pg_exact_fix1<EPI>(q, av, xv, pk, f, e);
+  } else {
+#pragma clang loop unroll(disable)
+    for (int q = 0; q < 16; ++q) pg_exact_fix1<EPI>(q, av, xv, pk, f, e);
+  }
 }
 
 // gelu_fast (nqk_numerics.h) on two values with packed f32 arithmetic (v_pk_fma / v_pk_mul:
@@ -186,6 +251,7 @@ __device__ __forceinline__ v2f gelu_fast2(v2f h) {
 // Q_LIM = (0.5 - 2^-126)(1 - 2^-23) rounded down: a rounded fma measure below it keeps the
 // exact one below 0.5 - 2^-126 (nqk_fused.hip quant_filter)
 constexpr float PG_QLIM = 0x1.fffffcp-2f;
+
 
 template <int EPI, int NK, bool F32X>
 __global__ void __launch_bounds__(256, 2)
@@ -313,6 +379,9 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       const float c1 = g3 == 0 ? e.c1[0] : (g3 == 1 ? e.c1[1] : e.c1[2]);
       const float k1 = g3 == 0 ? e.k1[0] : (g3 == 1 ? e.k1[1] : e.k1[2]);
       const float zp128 = g3 == 0 ? e.zp128[0] : (g3 == 1 ? e.zp128[1] : e.zp128[2]);
+      const float qlo = g3 == 0 ? e.qlo[0] : (g3 == 1 ? e.qlo[1] : e.qlo[2]);
+      const float qhi = g3 == 0 ? e.qhi[0] : (g3 == 1 ? e.qhi[1] : e.qhi[2]);
+      const float magic = g3 == 0 ? e.magic[0] : (g3 == 1 ? e.magic[1] : e.magic[2]);
       const float s_out = g3 == 0 ? e.s_out[0] : (g3 == 1 ? e.s_out[1] : e.s_out[2]);
       const double rs_out = g3 == 0 ? e.rs_out[0] : (g3 == 1 ? e.rs_out[1] : e.rs_out[2]);
       const double zp = g3 == 0 ? e.zp_out[0] : (g3 == 1 ? e.zp_out[1] : e.zp_out[2]);
@@ -352,92 +421,58 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         uint32_t pk[4] = {0, 0, 0, 0};
         uint32_t worst = 0;
         float hv[16];
+        v2f sprev;
         // the fast paths on element pairs (packed f32 arithmetic where an instruction exists)
 #pragma unroll
         for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) == 0; q += 2) {
           const v2f vf = v2f{(float)acc[i][q >> 2][q & 3], (float)acc[i][q >> 2][(q & 3) + 1]};
-          v2f rr;
+          v2f dd, sv;
           float m0, m1;
-          if constexpr (EPI == PG_QKV) {
+          if constexpr (EPI == PG_QKV) {  // (pg_round2 measured slower here: a longer dependent chain)
             const v2f u = __builtin_elementwise_fma(vf, v2f{c1, c1}, v2f{c2[q], c2[q + 1]});
-            rr = v2f{__builtin_rintf(u[0]), __builtin_rintf(u[1])};
-            const v2f dd = u - rr;
+            const v2f rr = v2f{__builtin_rintf(u[0]), __builtin_rintf(u[1])};
+            dd = u - rr;
             m0 = __builtin_fmaf(__builtin_fabsf(vf[0]), k1, __builtin_fabsf(dd[0]));
             m1 = __builtin_fmaf(__builtin_fabsf(vf[1]), k1, __builtin_fabsf(dd[1]));
+            const v2f b = rr + v2f{zp128, zp128};
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[0], 0.0f, 255.0f), q & 3, pk[q >> 2]);
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[1], 0.0f, 255.0f), (q & 3) + 1,
+                                                        pk[q >> 2]);
           } else {  // GELU: h exactly as the reference (F32X), then the filtered fast chain
             const v2f h = v2f{bias[q], bias[q + 1]} + vf * v2f{sacc, sacc};
             hv[q] = h[0];
             hv[q + 1] = h[1];
             const v2f tf = gelu_fast2(h) * v2f{rsf, rsf};
-            rr = v2f{__builtin_rintf(tf[0]), __builtin_rintf(tf[1])};
-            const v2f dd = tf - rr;
+            sv = round_magic2(tf, qlo, qhi, magic, dd);
             m0 = __builtin_fmaf(__builtin_fabsf(h[0]), e.g_rel, __builtin_fabsf(dd[0]));
             m1 = __builtin_fmaf(__builtin_fabsf(h[1]), e.g_rel, __builtin_fabsf(dd[1]));
           }
           worst = __builtin_elementwise_max(worst, __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
-          const v2f b = rr + v2f{zp128, zp128};
-          pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[0], e.lo128, e.hi128), q & 3, pk[q >> 2]);
-          pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[1], e.lo128, e.hi128), (q & 3) + 1,
-                                                      pk[q >> 2]);
-        }
-#pragma unroll
-        for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) != 0; ++q) {
-          const int a = acc[i][q >> 2][q & 3];
-          const float vf = (float)a;
-          float u;
-          if constexpr ((NQK_PG_DIAG & 2) != 0) {
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32((float)(a & 255), q & 3, pk[q >> 2]);
-            continue;
-          }
-          if constexpr (EPI == PG_QKV) {
-            u = __builtin_fmaf(vf, c1, c2[q]);
-            const float r = __builtin_rintf(u);
-            const float meas = __builtin_fmaf(__builtin_fabsf(vf), k1, __builtin_fabsf(u - r));
-            worst = __builtin_elementwise_max(worst, __float_as_uint(meas));
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, e.lo128, e.hi128), q & 3,
-                                                        pk[q >> 2]);
-          } else {  // GELU: h exactly as the reference (F32X), then the filtered fast chain
-            const float h = bias[q] + vf * sacc;
-            hv[q] = h;
-            const float tf = gelu_fast(h) * rsf;
-            const float r = __builtin_rintf(tf);
-            const float meas = __builtin_fmaf(__builtin_fabsf(h), e.g_rel, __builtin_fabsf(tf - r));
-            worst = __builtin_elementwise_max(worst, __float_as_uint(meas));
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(r + zp128, e.lo128, e.hi128), q & 3,
-                                                        pk[q >> 2]);
+          if constexpr (EPI != PG_QKV) {
+            if (q & 2) pk[q >> 2] = pack4_low(sprev, sv);
+            sprev = sv;
           }
         }
+        if constexpr (EPI == PG_QKV) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) pk[g] ^= 0x80808080u;
-        if constexpr ((NQK_PG_DIAG & 2) == 0) {
+          for (int g = 0; g < 4; ++g) pk[g] ^= 0x80808080u;  // offset bytes to two's complement
+        }
+#pragma unroll
+        for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) != 0; ++q)  // diagnostic: no epilogue math
+          pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32((float)(acc[i][q >> 2][q & 3] & 255), q & 3, pk[q >> 2]);
+        if constexpr ((NQK_PG_DIAG & 34) == 0) {  // (diagnostic 32: no exact fallback)
           if (__builtin_expect(__any(worst >= __float_as_uint(lim)), 0)) {
-            // the exact chain for every element the filter could not decide
+#if (NQK_PG_DIAG & 64)
+            if (lane == 0) atomicAdd(&g_pg_slow[0], 1ull);  // diagnostic: count exact-path entries
+#endif
+            int av[16];
+            float xv[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-              const int a = acc[i][q >> 2][q & 3];
-              const float vf = (float)a;
-              bool slow;
-              if constexpr (EPI == PG_QKV) {
-                const float u = __builtin_fmaf(vf, c1, c2[q]);
-                const float r = __builtin_rintf(u);
-                slow = !(__builtin_fmaf(__builtin_fabsf(vf), k1, __builtin_fabsf(u - r)) < lim);
-              } else {
-                const float tf = gelu_fast(hv[q]) * rsf;
-                const float r = __builtin_rintf(tf);
-                slow = !(__builtin_fmaf(__builtin_fabsf(hv[q]), e.g_rel, __builtin_fabsf(tf - r)) < lim);
-              }
-              if (__any(slow)) {
-                if (slow) {
-                  float y = bias[q] + vf * sacc;  // F32X: the f64 dequantize, exactly
-                  if constexpr (EPI == PG_GELU) {
-                    const float aa = ref_erf((float)((double)y * e.rdiv)) + e.add1;
-                    y = (y * aa) * e.mul2;
-                  }
-                  const int qv = pg_quant_exact(y, s_out, rs_out, zp, e.lo, e.hi);
-                  pk[q >> 2] = (pk[q >> 2] & ~(0xffu << (8 * (q & 3)))) | ((uint32_t)(qv & 0xff) << (8 * (q & 3)));
-                }
-              }
+              av[q] = acc[i][q >> 2][q & 3];
+              xv[q] = EPI == PG_QKV ? bias[q] : hv[q];
             }
+            pg_exact_fix<EPI>(av, xv, pk, PgFix{c1, k1, rsf, sacc, lim, s_out, rs_out, zp}, e);
           }
         }
         const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
@@ -595,6 +630,429 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------------
+// k_pg2: the epilogue of tile t - 1 runs INSIDE the k loop of tile t, in the same waves'
+// instruction streams (a SIMD overlaps a wave's own VALU with its MFMAs: tools/micro/fill.hip
+// 16x16x64 with 12 VALU per 32x32x32-equivalent runs at 0.55 of the MFMA-only rate, where the
+// two run back to back at ~0.35).  One 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N),
+// each 64 x 64 of a 128 x 256 tile: 64 accumulator registers for tile t and 64 holding tile
+// t - 1's results.  The A / B ring (4 stages of 24 KiB) runs continuously across tiles.
+// Per wave the epilogue is 4 units (M-subtiles of 16 rows x the wave's 64 columns, 16 values
+// per lane); unit u of tile t - 1 is spread over k steps SPU u .. SPU u + SPU - 1 of tile t
+// (SPU = NK / 4) in element pairs, its store at the end of its last step, the rounding
+// filter's exact fallback (rare, a wave-uniform branch) right after.  The first tile's k loop
+// runs the epilogue on no data through zero-size buffer descriptors (loads return 0, stores
+// are dropped); the last tile's epilogue runs after the loop.
+constexpr int P2_RD = 4, P2_PW = 3;             // ring stages; LDS-DMA ops per wave per stage
+constexpr int P2_COLP = P2_RD * PG_STG;         // 3 slots x (ct[256] | bias[256])
+constexpr int P2_TRS = P2_COLP + 3 * 2048;      // RESID: per-wave transpose scratch
+constexpr int P2_TR_ROW = 272;
+constexpr int p2_lds(int epi) { return P2_TRS + (epi == PG_RESID ? 8 * 16 * P2_TR_ROW : 0); }
+
+template <int EPI, int NK>
+struct P2Sched {  // the static per-k-step schedule (unit, phase, pairs per half)
+  static constexpr int SPU = NK / 4;
+  static constexpr int unit(int kt) { return kt / SPU; }
+  static constexpr int ph(int kt) { return kt % SPU; }
+  // element pairs [lo, hi) of the unit handled in half h (0 / 1) of step kt
+  static constexpr int plo(int kt, int h) { return 8 * (2 * ph(kt) + h) / (2 * SPU); }
+  static constexpr int phi(int kt, int h) { return 8 * (2 * ph(kt) + h + 1) / (2 * SPU); }
+  static constexpr bool last(int kt) { return ph(kt) == SPU - 1; }
+  // VMEM operations of the step besides the half-1 LDS-DMA: colp (step 1, start of half 2),
+  // RESID residual loads (phase 0, half 2), the unit's stores (last phase, half 2)
+  static constexpr int half2_ops(int kt) {
+    return (kt == 1 ? 1 : 0) + (EPI == PG_RESID && ph(kt) == 0 ? 4 : 0) + (last(kt) ? (EPI == PG_RESID ? 4 : 1) : 0);
+  }
+  static constexpr int m(int k) { return ((k % NK) + NK) % NK; }
+  // ops younger than stage g + 1 (issued in half 1 of step g - 2) at the middle of step g
+  static constexpr int younger(int kt) {
+    return half2_ops(m(kt - 2)) + P2_PW + half2_ops(m(kt - 1)) + P2_PW;
+  }
+};
+
+template <int EPI, int NK, bool F32X>
+__global__ void __launch_bounds__(512, 1)
+k_pg2(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
+      PgEpi e) {
+  static_assert(NK % P2_RD == 0 && NK % 4 == 0 && NK >= 8, "k_pg2: NK");
+  using S = P2Sched<EPI, NK>;
+  constexpr bool RESID = EPI == PG_RESID;
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int l15 = lane & 15, lg = lane >> 4;
+
+  const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X, jx = blockIdx.x / X;
+  const int nx = (G - x + X - 1) / X;
+  const int lo = (int)((int64_t)ntiles * x / X), hi = (int)((int64_t)ntiles * (x + 1) / X);
+  const int first = lo + jx;
+  if (first >= hi) return;
+  const int cnt = (hi - first + nx - 1) / nx;
+
+  constexpr int64_t BSTRIDE = (int64_t)NK * PG_BN * PG_BK;
+  const rsrc_t r_a = pg_rsrc(A, (uint32_t)((uint64_t)M * lda));
+  const rsrc_t r_b = pg_rsrc(Bp, (uint32_t)((uint64_t)tiles_n * BSTRIDE));
+  // LDS-DMA: A piece = wave (rows 16 w .. 16 w + 15), B pieces 2 w, 2 w + 1
+  const uint32_t va = (uint32_t)((16 * wave + (lane >> 2)) * lda + 16 * ((lane & 3) ^ pg_sw(lane >> 2)));
+  const uint32_t vb = (uint32_t)(2048 * wave + 16 * lane);
+  const int f_off = l15 * 64 + 16 * (lg ^ pg_sw(l15));
+
+  struct Src { uint32_t sa, sb; int r0, tn; };
+  auto src_of = [&](int it) __attribute__((always_inline)) {
+    Src s;
+    const int tile = first + (it < cnt ? it : cnt - 1) * nx;
+    const int tm = tile / tiles_n;
+    s.tn = tile - tm * tiles_n;
+    s.r0 = tm * PG_BM < M - PG_BM ? tm * PG_BM : M - PG_BM;
+    s.sa = (uint32_t)s.r0 * (uint32_t)lda;
+    s.sb = (uint32_t)((int64_t)s.tn * BSTRIDE);
+    return s;
+  };
+  auto issue_stage = [&](const Src& s, int kt, int slot) __attribute__((always_inline)) {
+    if constexpr ((NQK_PG_DIAG & 4) != 0) return;
+    int8_t* st = lds + slot * PG_STG;
+    pg_dma16(r_a, st + wave * 1024, va, s.sa + kt * PG_BK);
+    pg_dma16(r_b, st + PG_ASTG + (2 * wave) * 1024, vb, s.sb + (uint32_t)(kt * (PG_BN * PG_BK)));
+    pg_dma16(r_b, st + PG_ASTG + (2 * wave + 1) * 1024, vb, s.sb + (uint32_t)(kt * (PG_BN * PG_BK) + 1024));
+  };
+  // column constants of a tile (ct[256] | bias[256]): 256 B per wave, lanes 0..15
+  const rsrc_t r_ct = pg_rsrc(e.colterm, (uint32_t)((uint64_t)N * 4));
+  const rsrc_t r_bias = pg_rsrc(e.bias, e.bias ? (uint32_t)((uint64_t)N * 4) : 0u);
+  auto issue_colp = [&](int tn, int cslot) __attribute__((always_inline)) {
+    int8_t* dst = lds + P2_COLP + cslot * 2048 + wave * 256;
+    const uint32_t voff = (uint32_t)((tn * PG_BN + (wave & 3) * 64 + (lane & 15) * 4) * 4);
+    if (lane < 16) {
+      if (wave < 4) pg_dma16(r_ct, dst, voff, 0);
+      else pg_dma16(r_bias, dst, voff, 0);
+    }
+  };
+
+  v4i acc[4][4], accp[4][4];
+  v4i a01[2], a23[2], b0[4], b1[4], cinit[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accp[i][j] = v4i{0, 0, 0, 0};
+  const int8_t* const fa_base = lds + f_off + wm * 4096;
+  const int8_t* const fb_base = lds + f_off + wn * 4096;
+  auto rd_a = [&](v4i (&dst)[2], auto SLOT, auto I0, auto Q) __attribute__((always_inline)) {
+    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
+    constexpr int q = decltype(Q)::value;
+    dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + (decltype(I0)::value + q) * 1024>(fa_base);
+  };
+  auto rd_b = [&](v4i (&dst)[4], auto SLOT, auto Q) __attribute__((always_inline)) {
+    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
+    constexpr int q = decltype(Q)::value;
+    dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + PG_ASTG + q * 1024>(fb_base);
+  };
+  auto rd_cinit = [&](int cslot) __attribute__((always_inline)) {
+    const int8_t* cp = lds + P2_COLP + cslot * 2048;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      cinit[j] = pg_lds16(cp + (64 * wn + (RESID ? 16 * j + 4 * lg : 16 * lg + 4 * j)) * 4);
+  };
+
+  // ------------------------------------------------------------ the epilogue's state
+  // per tile (of tile t - 1, set at tile t's start): output descriptor (zero-size on the
+  // first tile), per-lane column constants, per-unit packed bytes / worst measure
+  struct EpiT {
+    rsrc_t out, res;
+    int r0, n0, g3;
+    float sacc, rsf, c1, k1, zp128, qlo, qhi, magic, lim;
+    int hh;
+  };
+  float ecol[16];  // QKV: c2 = RN(bias rsf); GELU: bias; RESID: bias of columns 4 ta .. + 3
+  uint32_t pk[4];
+  uint32_t worst = 0;
+  float hv[16];
+  v2f sprev;
+  v4u resv[4];
+  int8_t* const tr = lds + P2_TRS + wave * (16 * P2_TR_ROW);
+  const int ta = lane & 15, tb = lane >> 4;
+
+  auto epi_setup = [&](const Src& s, int cslot, bool valid) __attribute__((always_inline)) {
+    EpiT t;
+    t.r0 = s.r0;
+    t.n0 = s.tn * PG_BN;
+    const int cw = t.n0 + 64 * wn;
+    int g3 = 0;
+    if constexpr (EPI == PG_QKV) {
+      g3 = cw / e.group_cols;
+      g3 = g3 > 2 ? 2 : g3;
+    }
+    t.g3 = g3;
+    t.sacc = g3 == 0 ? e.sacc[0] : (g3 == 1 ? e.sacc[1] : e.sacc[2]);
+    t.rsf = g3 == 0 ? e.rsf[0] : (g3 == 1 ? e.rsf[1] : e.rsf[2]);
+    t.c1 = g3 == 0 ? e.c1[0] : (g3 == 1 ? e.c1[1] : e.c1[2]);
+    t.k1 = g3 == 0 ? e.k1[0] : (g3 == 1 ? e.k1[1] : e.k1[2]);
+    t.zp128 = g3 == 0 ? e.zp128[0] : (g3 == 1 ? e.zp128[1] : e.zp128[2]);
+    t.qlo = g3 == 0 ? e.qlo[0] : (g3 == 1 ? e.qlo[1] : e.qlo[2]);
+    t.qhi = g3 == 0 ? e.qhi[0] : (g3 == 1 ? e.qhi[1] : e.qhi[2]);
+    t.magic = g3 == 0 ? e.magic[0] : (g3 == 1 ? e.magic[1] : e.magic[2]);
+    void* op = g3 == 0 ? e.out[0] : (g3 == 1 ? e.out[1] : e.out[2]);
+    uint32_t obytes;
+    if constexpr (EPI == PG_QKV) obytes = (uint32_t)((uint64_t)((M + e.tokens - 1) / e.tokens) * e.tokens * e.heads * e.hdim);
+    else if constexpr (RESID) obytes = (uint32_t)((uint64_t)M * e.ldo * 4);
+    else obytes = (uint32_t)((uint64_t)M * e.ldo);
+    t.out = pg_rsrc(op, valid ? obytes : 0u);
+    t.res = pg_rsrc(RESID ? e.resid : nullptr, RESID && valid ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
+    t.hh = EPI == PG_QKV ? (cw - g3 * e.group_cols) / e.hdim : 0;
+    const int8_t* cp = lds + P2_COLP + cslot * 2048 + 1024;
+    if constexpr (RESID) {
+      const v4i bb = pg_lds16(cp + (64 * wn + 4 * ta) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ecol[r] = __int_as_float(bb[r]);
+      t.lim = 0.0f;
+    } else {
+      v4i bb[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bb[g] = pg_lds16(cp + (64 * wn + 16 * lg + 4 * g) * 4);
+      float cm = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float b = __int_as_float(bb[q >> 2][q & 3]);
+        if constexpr (EPI == PG_QKV) {
+          ecol[q] = b * t.rsf;
+          cm = __builtin_fmaxf(cm, __builtin_fabsf(ecol[q]));
+        } else {
+          ecol[q] = b;
+        }
+      }
+      t.lim = EPI == PG_QKV ? (PG_QLIM - cm * 0x1p-20f) - 0x1p-22f : e.g_lim;
+    }
+    return t;
+  };
+  // output offset of unit u's row (QKV: head layout; GELU: row-major int8)
+  auto unit_off = [&](const EpiT& t, int u) __attribute__((always_inline)) {
+    const int m = t.r0 + 64 * wm + 16 * u + l15;
+    if constexpr (EPI == PG_QKV) {
+      const int img = m / e.tokens, tt = m - img * e.tokens;
+      return (uint32_t)(((img * e.heads + t.hh) * e.tokens + tt) * e.hdim + 16 * lg);
+    } else {
+      return (uint32_t)(m * e.ldo + t.n0 + 64 * wn + 16 * lg);
+    }
+  };
+  auto res_off = [&](const EpiT& t, int u, int k) __attribute__((always_inline)) {
+    return (uint32_t)(((t.r0 + 64 * wm + 16 * u + 4 * k + tb) * e.ldo + t.n0 + 64 * wn + 4 * ta) * 4);
+  };
+  // the fast path of element pairs [p0, p1) of unit u (int8-output epilogues)
+  auto epi_pairs = [&](const EpiT& t, auto U, int p0, int p1) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
+    if constexpr ((NQK_PG_DIAG & 2) != 0) return;  // diagnostic: no epilogue math
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      if (p < p0 || p >= p1) continue;
+      const int q = 2 * p;
+      const v2f vf = v2f{(float)accp[u][q >> 2][q & 3], (float)accp[u][q >> 2][(q & 3) + 1]};
+      v2f dd, sv;
+      float m0, m1;
+      if constexpr (EPI == PG_QKV) {
+        const v2f uu = __builtin_elementwise_fma(vf, v2f{t.c1, t.c1}, v2f{ecol[q], ecol[q + 1]});
+        const v2f rr = v2f{__builtin_rintf(uu[0]), __builtin_rintf(uu[1])};
+        dd = uu - rr;
+        m0 = __builtin_fmaf(__builtin_fabsf(vf[0]), t.k1, __builtin_fabsf(dd[0]));
+        m1 = __builtin_fmaf(__builtin_fabsf(vf[1]), t.k1, __builtin_fabsf(dd[1]));
+        const v2f b = rr + v2f{t.zp128, t.zp128};
+        pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[0], 0.0f, 255.0f), q & 3, pk[q >> 2]);
+        pk[q >> 2] =
+            __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[1], 0.0f, 255.0f), (q & 3) + 1, pk[q >> 2]);
+      } else {
+        const v2f h = v2f{ecol[q], ecol[q + 1]} + vf * v2f{t.sacc, t.sacc};
+        hv[q] = h[0];
+        hv[q + 1] = h[1];
+        const v2f tf = gelu_fast2(h) * v2f{t.rsf, t.rsf};
+        sv = round_magic2(tf, t.qlo, t.qhi, t.magic, dd);
+        m0 = __builtin_fmaf(__builtin_fabsf(h[0]), e.g_rel, __builtin_fabsf(dd[0]));
+        m1 = __builtin_fmaf(__builtin_fabsf(h[1]), e.g_rel, __builtin_fabsf(dd[1]));
+      }
+      worst = __builtin_elementwise_max(worst, __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
+      if constexpr (EPI != PG_QKV) {
+        if (q & 2) pk[q >> 2] = pack4_low(sprev, sv);
+        sprev = sv;
+      }
+    }
+  };
+  // end of unit u (int8 outputs): the rounding filter's exact fallback for the elements it
+  // could not decide (rare: a wave-uniform branch), bytes to two's complement, the store
+  auto epi_finish = [&](const EpiT& t, int cslot, auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
+    if constexpr (EPI == PG_QKV) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pk[g] ^= 0x80808080u;
+    }
+    if (__builtin_expect(__any(worst >= __float_as_uint(t.lim)), 0) && (NQK_PG_DIAG & 32) == 0) {
+      const float s_out = t.g3 == 0 ? e.s_out[0] : (t.g3 == 1 ? e.s_out[1] : e.s_out[2]);
+      const double rs_out = t.g3 == 0 ? e.rs_out[0] : (t.g3 == 1 ? e.rs_out[1] : e.rs_out[2]);
+      const double zp = t.g3 == 0 ? e.zp_out[0] : (t.g3 == 1 ? e.zp_out[1] : e.zp_out[2]);
+      const int8_t* bp = lds + P2_COLP + cslot * 2048 + 1024 + (64 * wn + 16 * lg) * 4;
+      int av[16];
+      float xv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        av[q] = accp[u][q >> 2][q & 3];
+        xv[q] = EPI == PG_QKV ? *reinterpret_cast<const float*>(bp + 4 * q) : hv[q];
+      }
+      pg_exact_fix<EPI>(av, xv, pk, PgFix{t.c1, t.k1, t.rsf, t.sacc, t.lim, s_out, rs_out, zp}, e);
+    }
+    const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
+    if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
+    else __builtin_amdgcn_raw_buffer_store_b128(st, t.out, unit_off(t, u), 0, 0);
+  };
+  // RESID unit u: residual loads (phase 0), then (last phase) the transposed accumulators
+  // through the wave's LDS scratch, y = (bias + RN(v sacc)) + residual, whole-line stores
+  auto res_load = [&](const EpiT& t, auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) resv[k] = pg_load16(t.res, res_off(t, u, k), 0u);
+  };
+  auto res_unit = [&](const EpiT& t, auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value;
+    if constexpr ((NQK_PG_DIAG & 2) != 0) {  // diagnostic: no epilogue math / LDS transpose
+      const v4u st = v4u{resv[0][0], resv[1][1], resv[2][2], resv[3][3]} ^ (v4u)accp[u][0];
+      if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
+      else __builtin_amdgcn_raw_buffer_store_b128(st, t.out, res_off(t, u, 0), 0, 0);
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<v4i*>(tr + l15 * P2_TR_ROW + (16 * j + 4 * lg) * 4) = accp[u][j];
+    v4i tv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tv[k] = *reinterpret_cast<const v4i*>(tr + (4 * k + tb) * P2_TR_ROW + 16 * ta);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v4u st;
+      if constexpr (F32X) {
+        const v2f d01 = v2f{(float)tv[k][0], (float)tv[k][1]} * v2f{t.sacc, t.sacc};
+        const v2f d23 = v2f{(float)tv[k][2], (float)tv[k][3]} * v2f{t.sacc, t.sacc};
+        const v2f y01 = (v2f{ecol[0], ecol[1]} + d01) + v2f{__uint_as_float(resv[k][0]), __uint_as_float(resv[k][1])};
+        const v2f y23 = (v2f{ecol[2], ecol[3]} + d23) + v2f{__uint_as_float(resv[k][2]), __uint_as_float(resv[k][3])};
+        st = v4u{__float_as_uint(y01[0]), __float_as_uint(y01[1]), __float_as_uint(y23[0]), __float_as_uint(y23[1])};
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = (float)((double)tv[k][r] * (double)t.sacc);
+          st[r] = __float_as_uint((ecol[r] + d) + __uint_as_float(resv[k][r]));
+        }
+      }
+      if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
+      else __builtin_amdgcn_raw_buffer_store_b128(st, t.out, res_off(t, u, k), 0, 0);
+    }
+  };
+
+  // ------------------------------------------------------------ MFMA half steps
+  // 8 MFMAs (M-subtiles 2 h, 2 h + 1 x the 4 N-subtiles); the caller's other work of the
+  // half is in the same scheduling region, so the compiler places it between the MFMAs
+  auto mfma_half = [&](auto H, auto FIRST, const v4i (&aa)[2], const v4i (&bb)[4]) __attribute__((always_inline)) {
+    constexpr int h = decltype(H)::value;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int ii = q >> 2, j = q & 3;
+      if constexpr (decltype(FIRST)::value)
+        acc[2 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], cinit[j], 0, 0, 0);
+      else
+        acc[2 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], acc[2 * h + ii][j], 0, 0, 0);
+    }
+  };
+
+  // ------------------------------------------------------------ prologue
+  Src cur = src_of(0);
+  issue_colp(cur.tn, 0);
+  issue_stage(cur, 0, 0);
+  issue_stage(cur, 1, 1);
+  issue_stage(cur, 2, 2);
+  pg_vmcnt<2 * P2_PW>();  // stage 0 and the column constants landed (stages 1, 2 may fly)
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  sfor<0, 2>([&](auto Q) __attribute__((always_inline)) { rd_a(a01, ic<0>{}, ic<0>{}, Q); });
+  sfor<0, 4>([&](auto Q) __attribute__((always_inline)) { rd_b(b0, ic<0>{}, Q); });
+  rd_cinit(0);
+  EpiT et = epi_setup(cur, 0, false);  // no previous tile: zero-size descriptors
+
+  for (int it = 0; it < cnt; ++it) {
+    const Src nxt = src_of(it + 1);  // = cur's source for the last tile (re-staged, never read)
+    const int cs = it % 3, cs_prev = (it + 2) % 3, cs_next = (it + 1) % 3;
+    if (it > 0) et = epi_setup(src_of(it - 1), cs_prev, true);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cinit[j] = -cinit[j];
+    sfor<0, NK>([&](auto KT) __attribute__((always_inline)) {
+      constexpr int kt = decltype(KT)::value;
+      constexpr int slot = kt % P2_RD;
+      constexpr int u = S::unit(kt);
+      v4i(&bc)[4] = (kt & 1) ? b1 : b0;
+      v4i(&bn)[4] = (kt & 1) ? b0 : b1;
+      // ---- half 1: subtiles 0, 1; the A fragments of subtiles 2, 3; stage kt + 3 (this
+      // tile's, or the next tile's first three); the epilogue's first pairs of the step
+      if constexpr (EPI != PG_RESID)
+        if constexpr (S::ph(kt) == 0) {
+          worst = 0;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) pk[g] = 0;
+        }
+      mfma_half(ic<0>{}, std::integral_constant<bool, kt == 0>{}, a01, bc);
+      rd_a(a23, ic<slot>{}, ic<2>{}, ic<0>{});
+      rd_a(a23, ic<slot>{}, ic<2>{}, ic<1>{});
+      if constexpr (kt + 3 < NK) issue_stage(cur, kt + 3, (kt + 3) % P2_RD);
+      else issue_stage(nxt, kt + 3 - NK, (kt + 3) % P2_RD);
+      if constexpr (EPI != PG_RESID) epi_pairs(et, ic<u>{}, S::plo(kt, 0), S::phi(kt, 0));
+      // ---- middle: stage kt + 1 landed (exact count of younger VMEM operations; the
+      // first tile's first steps follow the prologue instead of a previous tile)
+      if constexpr (kt < 2) {
+        if (it == 0) {
+          if constexpr (kt == 0) pg_vmcnt<P2_PW + P2_PW>();
+          else pg_vmcnt<S::half2_ops(0) + P2_PW + P2_PW>();
+        } else {
+          pg_vmcnt<S::younger(kt)>();
+        }
+      } else {
+        pg_vmcnt<S::younger(kt)>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- half 2: subtiles 2, 3; the next step's fragments (and at the tile's end the
+      // next tile's initial accumulators); colp of the next tile (step 1); the epilogue
+      if constexpr (kt == 1) issue_colp(nxt.tn, cs_next);
+      if constexpr (EPI == PG_RESID && S::ph(kt) == 0) res_load(et, ic<u>{});
+      mfma_half(ic<1>{}, std::integral_constant<bool, kt == 0>{}, a23, bc);
+      rd_a(a01, ic<(kt + 1) % P2_RD>{}, ic<0>{}, ic<0>{});
+      rd_a(a01, ic<(kt + 1) % P2_RD>{}, ic<0>{}, ic<1>{});
+      sfor<0, 4>([&](auto Q) __attribute__((always_inline)) { rd_b(bn, ic<(kt + 1) % P2_RD>{}, Q); });
+      if constexpr (kt == NK - 1) rd_cinit(cs_next);
+      if constexpr (EPI != PG_RESID) {
+        epi_pairs(et, ic<u>{}, S::plo(kt, 1), S::phi(kt, 1));
+        if constexpr (S::last(kt)) epi_finish(et, cs_prev, ic<u>{});
+      } else {
+        if constexpr (S::last(kt)) res_unit(et, ic<u>{});
+      }
+    });
+    // tile it's results become the previous tile's
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accp[i][j] = acc[i][j];
+    cur = nxt;
+  }
+  // the last tile's epilogue (nothing left to overlap with)
+  {
+    const int it = cnt;
+    et = epi_setup(src_of(it - 1), (it + 2) % 3, true);
+    sfor<0, 4>([&](auto U) __attribute__((always_inline)) {
+      if constexpr (EPI == PG_RESID) {
+        res_load(et, U);
+        res_unit(et, U);
+      } else {
+        worst = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pk[g] = 0;
+        epi_pairs(et, U, 0, 8);
+        epi_finish(et, (it + 2) % 3, U);
+      }
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // weight image of k_pg: [N / 256][K / 64] stages of 256 rows x 64 B in the LDS order of the
 // stage (row rho: column 64 (rho >> 6) + pg_bperm(rho & 63) of the panel; physical chunk
 // pc: logical chunk pc ^ pg_sw(rho)); columns past N are zero
@@ -638,8 +1096,9 @@ static int pg_num_cus() {
   return n;
 }
 
-// Launches k_pg for one projection GEMM when it takes the case; returns 1 if launched, 0
-// if the caller must use another kernel, < 0 on error.  bp: the nqk_pack_pg image.
+// Launches k_pg2 (or k_pg) for one projection GEMM when it takes the case; returns the
+// kernel id for nqk_qgemm_last_kernel (5 k_pg2, 4 k_pg) if launched, 0 if the caller must
+// use another kernel, < 0 on error.  bp: the nqk_pack_pg image.
 int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, int64_t K, int64_t lda,
               const nqk_epilogue* p, bool f32x) {
   if (getenv("NQK_NO_PG")) return 0;
@@ -650,9 +1109,8 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   if ((epi == PG_QKV || epi == PG_GELU) && (!f32x || K != 768)) return 0;
   if (epi == PG_QKV && !(p->hdim == 64 && p->group_cols % 64 == 0 && (double)M * p->heads * p->hdim < 2147483647.0))
     return 0;
-  // the residual epilogues stay on k_qgemm_big unless NQK_PG_RESID=1 (k_pg measured slower
-  // there: profiles/r03_pg_micro.txt)
-  if (epi == PG_RESID && (!getenv("NQK_PG_RESID") || p->resid == nullptr || (M % PG_BM != 0 && p->resid == p->out[0])))
+  // NQK_PG_NORESID=1 keeps the residual epilogues on k_qgemm_big (the round-2 kernel)
+  if (epi == PG_RESID && (getenv("NQK_PG_NORESID") || p->resid == nullptr || (M % PG_BM != 0 && p->resid == p->out[0])))
     return 0;
   if (epi == PG_GELU && !(p->div == 1.41421354f && p->add1 == 1.0f && p->mul2 == 0.5f)) return 0;
   auto al16 = [](const void* q) { return q == nullptr || (((uintptr_t)q) & 15) == 0; };
@@ -673,6 +1131,9 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     e.c1[g] = e.sacc[g] * e.rsf[g];
     e.k1[g] = __builtin_fabsf(e.c1[g]) * 0x1p-21f;
     e.zp128[g] = (float)p->zp_out[gg] + 128.0f;
+    e.qlo[g] = -128.0f - (float)p->zp_out[gg];
+    e.qhi[g] = 127.0f - (float)p->zp_out[gg];
+    e.magic[g] = 0x1.8p23f + (float)p->zp_out[gg];
     e.out[g] = p->out[gg];
     if (epi != PG_RESID) {
       if (!(__builtin_fabsf(s_out) >= 0x1p-100f && __builtin_fabsf(s_out) <= 0x1p100f)) return 0;
@@ -684,8 +1145,6 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   e.colterm = p->colterm;
   e.lo = -128.0;
   e.hi = 127.0;
-  e.lo128 = 0.0f;
-  e.hi128 = 255.0f;
   e.group_cols = p->group_cols > 0 ? p->group_cols : (int)N;
   e.tokens = p->tokens;
   e.heads = p->heads;
@@ -699,12 +1158,35 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     // the GELU filter of nqk_fused.hip make_epi: |gelu_fast - gelu| <= GELU_REL |h| +
     // GELU_ABS, plus the product t = y * rsf
     const double ars = __builtin_fabs(1.0 / (double)p->s_out[0]) * 1.02;
-    e.g_rel = (float)((double)GELU_REL * 1.27 * ars);
+    e.g_rel = (float)(((double)GELU_REL + 0x1.13p-22) * ars);
     const float g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
     e.g_lim = (float)((0.5 - (double)g_abs) * (1.0 - 0x1p-22));
   }
   const int tiles_n = (int)(N / PG_BN), tiles_m = (int)((M + PG_BM - 1) / PG_BM);
   const int nt = tiles_m * tiles_n;
+  // k_pg (two workgroups per CU, epilogue after the k loop) by default; NQK_PG_KERNEL=2
+  // selects k_pg2 (epilogue inside the next tile's k loop, one workgroup per CU), measured
+  // slower (its interleaved epilogue does not hide behind the MFMAs)
+  const char* kv = getenv("NQK_PG_KERNEL");
+  if (kv && atoi(kv) == 2) {
+    const int grid2 = nt < pg_num_cus() ? nt : pg_num_cus();
+    const int key2 = epi * 4 + (K == 3072 ? 2 : 0) + (f32x ? 1 : 0);
+    switch (key2) {
+#define PG2L(E, NKV, X)                                                                                           \
+  case E * 4 + (NKV == 48 ? 2 : 0) + (X ? 1 : 0):                                                                 \
+    hipLaunchKernelGGL((k_pg2<E, NKV, X>), dim3(grid2), dim3(512), p2_lds(E), stream(), a, bp, (int)M, (int)N,    \
+                       (int)lda, tiles_n, nt, e);                                                                 \
+    break;
+      PG2L(PG_QKV, 12, true)
+      PG2L(PG_GELU, 12, true)
+      PG2L(PG_RESID, 12, true) PG2L(PG_RESID, 12, false) PG2L(PG_RESID, 48, true) PG2L(PG_RESID, 48, false)
+#undef PG2L
+      default:
+        return 0;
+    }
+    const int rc2 = launch_status("nqk_qgemm_fused(pg2)");
+    return rc2 < 0 ? rc2 : 5;
+  }
   const int slots = 2 * pg_num_cus();
   const int grid = nt < slots ? nt : slots;
   // initial delay of the second workgroup per CU, in units of s_sleep 8 (~512 cycles)
@@ -725,7 +1207,7 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
       return 0;
   }
   const int rc = launch_status("nqk_qgemm_fused(pg)");
-  return rc < 0 ? rc : 1;
+  return rc < 0 ? rc : 4;
 }
 
 }  // namespace nqk

@@ -17,7 +17,7 @@ def _last_kernel():
     return _lib.load().nqk_qgemm_last_kernel()
 
 
-def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed):
+def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, kernel=2):
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray
     from numpy_quant.plan import EPI_GELU, EPI_QKV, EPI_RESID, _gemm, _pack_b, _pack_pg
@@ -35,10 +35,10 @@ def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed):
     assert pg is not None
     zpa = -5
     colterm = DeviceArray.from_host((col_h * zpa).astype(np.int32))
-    for k in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_NO_PG"):
+    for k in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_NO_PG", "NQK_PG_NORESID"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("NQK_NO_PROJ", "1")
-    monkeypatch.setenv("NQK_PG_RESID", "1")  # opt-in for the residual epilogues
+    monkeypatch.setenv("NQK_PG_KERNEL", str(kernel))
     if no_f32x:
         monkeypatch.setenv("NQK_NO_F32X", "1")
     e = _lib.Epilogue()
@@ -104,11 +104,14 @@ def _numpy_ref(epi_name, M, N, K, host):
     ("resid", 128 * 197, 768, 3072, 1.0, True), ("resid", 300, 768, 768, 1.0, False),
     ("resid", 256 * 197, 768, 3072, 1.0, False),
 ])
-def test_pg_gemm_equals_big_tile(epi_name, M, N, K, s_out_scale, no_f32x, monkeypatch):
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_pg_gemm_equals_big_tile(epi_name, M, N, K, s_out_scale, no_f32x, kernel, monkeypatch):
+    """kernel 1: k_pg (two workgroups per CU); 2: k_pg2 (the epilogue of each tile inside
+    the next tile's k loop)."""
     seed = M + N + K
-    k0, ref, host = _run(epi_name, M, N, K, s_out_scale, False, no_f32x, monkeypatch, seed)
-    k1, got, _ = _run(epi_name, M, N, K, s_out_scale, True, no_f32x, monkeypatch, seed)
-    assert (k0, k1) == (1, 4), (k0, k1)
+    k0, ref, host = _run(epi_name, M, N, K, s_out_scale, False, no_f32x, monkeypatch, seed, kernel)
+    k1, got, _ = _run(epi_name, M, N, K, s_out_scale, True, no_f32x, monkeypatch, seed, kernel)
+    assert (k0, k1) == (1, 3 + kernel), (k0, k1)
     if M <= 1024:
         npref = _numpy_ref(epi_name, M, N, K, host)
         if npref is not None:

@@ -22,7 +22,6 @@ from numpy_quant import _lib  # noqa: E402
 from numpy_quant.device import DeviceArray  # noqa: E402
 from numpy_quant.plan import _pack_b, _pack_pg  # noqa: E402
 
-os.environ.setdefault("NQK_PG_RESID", "1")
 _lib.ensure_init()
 main = _lib.load()
 M = int(os.environ.get("GM_M", 256 * 197))
@@ -96,11 +95,19 @@ def timed(lib, epi, a, bt, N, K, e, env):
             lib.nqk_last_error.restype = ctypes.c_char_p
             raise RuntimeError(f"nqk_qgemm_fused rc={rc}: {lib.nqk_last_error().decode()}")
         sync_all()
+        diag = getattr(lib, "nqk_pg_diag_slow", None) if hasattr(lib, "nqk_pg_diag_slow") else None
+        if diag is not None:
+            diag.restype = ctypes.c_ulonglong
+            diag(1)
         t0 = time.perf_counter()
         for _ in range(REPS):
             lib.nqk_qgemm_fused(*args)
         lib.nqk_sync()
-        return (time.perf_counter() - t0) / REPS * 1e6
+        dt = (time.perf_counter() - t0) / REPS * 1e6
+        if diag is not None:
+            steps = M * N / 1024
+            print(f"  exact-path entries per launch: {diag(0) / REPS:.0f} of {steps:.0f} epilogue steps", flush=True)
+        return dt
     finally:
         for k, v in old.items():
             if v is None:
@@ -118,6 +125,7 @@ for name in sel:
         variants.append((f"pg:{lname}", lib, {}, True))
     for vname, env in envs.items():
         variants.append((f"pg:{vname}", main, env, True))
+    variants.append(("pg2", main, {"NQK_PG_KERNEL": "2"}, True))
     variants.append(("r02", main, {"NQK_PROJ_GELU": "1"} if epi == 4 else {}, False))
     res = {v[0]: [] for v in variants}
     for _ in range(ROUNDS):
