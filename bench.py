@@ -127,7 +127,7 @@ def build_vit(batch: int, bit_width: int, group, calib_batch: int = 8, tiny: boo
 
 
 VIT_TINY = (192, 3, 768)  # ViT-Ti/16: width, heads, MLP width (head size 64 and depth 12 as ViT-Base)
-PROJ_TAGS = ("qgemm_qkv", "qgemm_resid", "qgemm_gelu")  # MatMuls with constant weights (k_proj / k_qgemm_big)
+PROJ_TAGS = ("qgemm_qkv", "qgemm_resid", "qgemm_gelu")  # MatMuls with constant weights (k_pg)
 
 
 def kernel_breakdown(qmodel, x_dev):
@@ -319,10 +319,11 @@ def run_vit(args, group):
     res["matmul_tops"] = round(achieved, 2)
     res["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(INT8_PEAK_TOPS, 1),
                        "unit": "TOPS", "frac": round(achieved / INT8_PEAK_TOPS, 4),
-                       "traffic": traffic_from_profiles(("k_proj", "k_qgemm_big")) if bw == 8 else None,
-                       "kernel": "the 48 int8 MFMA projection GEMMs of one forward, fused epilogues: k_proj "
-                                 "(persistent 256x256 tiles: QKV) and k_qgemm_big (FFN up + GELU, attention output, "
-                                 "FFN down + residual); 2*M*N*K int8 ops per launch",
+                       "traffic": traffic_from_profiles(("k_pg",)) if bw == 8 else None,
+                       "kernel": "the 48 int8 MFMA projection GEMMs of one forward, fused epilogues: k_pg "
+                                 "(persistent 128x256 tiles, v_mfma_i32_16x16x64_i8, two workgroups per CU) for "
+                                 "QKV + head split, FFN up + GELU, attention output + residual, FFN down + "
+                                 "residual; 2*M*N*K int8 ops per launch",
                        "launches": proj["launches"], "avg_launch_us": round(1e3 * proj["ms"] / max(1, proj["launches"]), 2),
                        "gemm_ms_per_forward": round(proj["ms"], 3)}
     res["kernels"] = kern

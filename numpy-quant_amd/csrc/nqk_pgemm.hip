@@ -59,6 +59,13 @@ constexpr int PG_PW = 2 + 4;                      // LDS-DMA pieces per wave per
 
 enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fused.hip
 
+#ifndef NQK_PG_STAUX
+#define NQK_PG_STAUX 0  // cache-policy bits of the epilogue's output stores (16 = sc1: the line leaves L2)
+#endif
+#ifndef NQK_PG_PRIO
+#define NQK_PG_PRIO 0  // 1: s_setprio 1 in the k loop, 0 in the epilogue; 2: static prio 1 for the second
+                       // workgroup of a CU; 3: prio 1 in the epilogue, 0 in the k loop
+#endif
 #ifndef NQK_PG_DIAG
 #define NQK_PG_DIAG 0  // diagnostic builds only (tools/pg_diag.sh): 1 = no epilogue stores,
                        // 2 = trivial epilogue math, 4 = no operand loads, 8 = no barriers,
@@ -477,7 +484,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         }
         const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
         if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, off, 0, NQK_PG_STAUX);
       });
     }
   };
@@ -536,7 +543,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
           }
         }
         if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, res_off(s, i, k), 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, res_off(s, i, k), 0, NQK_PG_STAUX);
       }
       if constexpr (i + 2 < 8) res_issue(s, ic<i + 2>{});
     });
@@ -553,7 +560,12 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   issue_colp(cur.tn, 0);
   issue_stage(cur, 0, 0);
   issue_stage(cur, 1, 1);
+  if constexpr (NQK_PG_PRIO == 2) {
+    if ((int)blockIdx.x >= G / 2) __builtin_amdgcn_s_setprio(1);
+  }
   for (int it = 0; it < cnt; ++it) {
+    if constexpr (NQK_PG_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(0);
     const bool more = it + 1 < cnt;
     const Src nxt = src_of(first + (more ? it + 1 : it) * nx);
     const int cs = it & 1;
@@ -623,6 +635,8 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     issue_stage(nxt, 0, 0);
     issue_stage(nxt, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NQK_PG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(1);
     if constexpr (RESID) epilogue_resid(cur, cs);
     else epilogue(cur, cs);
     cur = nxt;
