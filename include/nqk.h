@@ -155,6 +155,13 @@ int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch, int64_t M
  * of the NumPy being matched. */
 int nqk_sgemv_t(const float* x, const float* bt, float* y, int64_t N, int64_t K, int64_t ldb, int64_t threads);
 
+/* The other one-row products of NumPy's matmul (model.py:122-131 Gemm / tensor.py:100-101
+ * FTensor.matmul on one row): N == 1 (cblas_sdot: f32 products summed in double, restated
+ * for K < 32) and K in 2..8 except 4 (OpenBLAS's small-m GEMV-T kernels: fma chains on
+ * column blocks, multiply-add chains on leftover columns; see k_sgemv_small for the parts
+ * not restated).  Same operand layout as nqk_sgemv_t; for N == 1 bt is the K-vector. */
+int nqk_sgemv_small(const float* x, const float* bt, float* y, int64_t N, int64_t K, int64_t ldb);
+
 /* im2col for Conv (numpy_helper.py:18-70): x NCHW f32 -> cols[N*Ho*Wo][KH*KW*C]
  * (column order kh, kw, c), zero padding pads = (ph0, pw0, ph1, pw1). */
 /* ViT patch embedding in one GEMM (plan.py FusedEmbed): Conv as im2col . W in the BLAS

@@ -527,6 +527,9 @@ k_sgemv_t(const float* __restrict__ x, const float* __restrict__ bt, float* __re
     } else if (cls == 1) {  // lanes 0-3: rows r = l mod 4, multiply then add
       if (l < 4)
         for (; i < nb; i += 4) acc = acc + xb[i + l] * a[i + l];
+    } else if (K == 4) {  // K = 4: the single leftover column is one multiply-add chain
+      if (l == 0)         // (identified against np.matmul: tests/test_host.py)
+        for (; i < nb; ++i) acc = acc + xb[i] * a[i];
     } else {  // lane l: set l / 4, row l % 4 of each 8-row step (prologue rows to set 0)
       if (nb & 4) {
         if (l < 4) acc = acc + xb[l] * a[l];
@@ -556,6 +559,51 @@ k_sgemv_t(const float* __restrict__ x, const float* __restrict__ bt, float* __re
     }
   }
   if (live && l == 0) y[j] = yv;
+}
+
+// One-row products OpenBLAS does not send through the GEMV-T kernels above (identified
+// against np.matmul, oracle/openblas_order.py sgemv_small / sdot, pinned by
+// tests/test_host.py):
+//  * N == 1 (NumPy's matmul takes cblas_sdot for a 1 x 1 result): below 32 rows the
+//    f32 products are summed in double, in order, and the sum rounded once to f32;
+//  * K in 2..8 except 4 (the AVX-512 small-m GEMV-T kernels): columns in blocks of 16
+//    (K = 2), 4 (K = 5) or 8 (K = 3, 6, 7) are k-ordered fma chains; the columns left over
+//    are multiply-add chains, except a leftover 4-column block for K = 3, 6, 7 and a last
+//    odd column for K = 3 (orders not restated: computed as fma chains; the host reports
+//    them, kernels.one_row_restated) and K = 8 (not restated at all).
+__global__ void __launch_bounds__(256)
+k_sgemv_small(const float* __restrict__ x, const float* __restrict__ bt, float* __restrict__ y, int64_t N, int64_t K,
+              int64_t ldb) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  const float* w = bt + j * ldb;
+  if (N == 1) {
+    double d = 0.0;
+    for (int64_t k = 0; k < K; ++k) {
+      const float p = x[k] * w[k];  // -ffp-contract=off: the f32 product, then the double add
+      d += (double)p;
+    }
+    y[0] = (float)d;
+    return;
+  }
+  const int64_t blk = K == 2 ? 16 : (K == 5 ? 4 : 8);
+  const int64_t f_end = N / blk * blk;
+  bool chain_fma = j < f_end || K == 8;
+  if (!chain_fma && (K == 3 || K == 6 || K == 7)) {
+    int64_t r = N - f_end, loc = j - f_end;
+    if (r >= 4) {
+      if (loc < 4) chain_fma = true;  // the 4-column block (not restated)
+      r -= 4;
+      loc -= 4;
+    }
+    if (!chain_fma && K == 3 && !((r & 2) && loc < 2)) chain_fma = true;  // K = 3: last odd column
+  }
+  float acc = 0.0f;
+  if (chain_fma)
+    for (int64_t k = 0; k < K; ++k) acc = __builtin_fmaf(x[k], w[k], acc);
+  else
+    for (int64_t k = 0; k < K; ++k) acc = acc + x[k] * w[k];
+  y[j] = acc;
 }
 
 }  // namespace
@@ -716,4 +764,13 @@ extern "C" int nqk_sgemv_t(const float* x, const float* bt, float* y, int64_t N,
   const int64_t lanes = N * 8;
   hipLaunchKernelGGL(k_sgemv_t, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream(), x, bt, y, N, K, ldb, t);
   return launch_status("nqk_sgemv_t");
+}
+
+extern "C" int nqk_sgemv_small(const float* x, const float* bt, float* y, int64_t N, int64_t K, int64_t ldb) {
+  if (N <= 0) return 0;
+  if (K <= 0) return fail("nqk_sgemv_small: K >= 1 expected");
+  if (ldb < K) return fail("nqk_sgemv_small: ldb < K");
+  if (N > 1 && !(K >= 2 && K <= 8 && K != 4)) return fail("nqk_sgemv_small: N == 1, or K in 2..8 except 4 expected");
+  hipLaunchKernelGGL(k_sgemv_small, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream(), x, bt, y, N, K, ldb);
+  return launch_status("nqk_sgemv_small");
 }

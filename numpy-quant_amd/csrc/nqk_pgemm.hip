@@ -60,11 +60,17 @@ constexpr int PG_PW = 2 + 4;                      // LDS-DMA pieces per wave per
 enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fused.hip
 
 #ifndef NQK_PG_STAUX
-#define NQK_PG_STAUX 0  // cache-policy bits of the epilogue's output stores (16 = sc1: the line leaves L2)
+#define NQK_PG_STAUX 2  // cache-policy bits of the epilogue's output stores: nt (profiles/r03c_*: out-proj
+                        // 77 -> 60 us; 16 = sc1, the line leaves L2: no gain)
+#endif
+#ifndef NQK_PG_RLAUX
+#define NQK_PG_RLAUX -1  // cache-policy bits of the RESID epilogue's residual loads: -1 = nt for K = 3072
+                         // (FFN-down 144 -> 138 us) and plain for K = 768 (nt: out-proj 59 -> 70 us)
 #endif
 #ifndef NQK_PG_PRIO
-#define NQK_PG_PRIO 0  // 1: s_setprio 1 in the k loop, 0 in the epilogue; 2: static prio 1 for the second
-                       // workgroup of a CU; 3: prio 1 in the epilogue, 0 in the k loop
+#define NQK_PG_PRIO 3  // 3: s_setprio 1 in the epilogue, 0 in the k loop (the epilogue's VALU ahead of the
+                       // other workgroup's k loop on the SIMD: -2..-4 %, profiles/r03c_*); 1: the reverse;
+                       // 2: static prio 1 for the second workgroup of a CU; 0: none
 #endif
 #ifndef NQK_PG_DIAG
 #define NQK_PG_DIAG 0  // diagnostic builds only (tools/pg_diag.sh): 1 = no epilogue stores,
@@ -148,8 +154,12 @@ __device__ __forceinline__ void pg_vmcnt() {
   __builtin_amdgcn_sched_barrier(0);
 }
 // 16-byte buffer load to VGPRs (compiler-visible: it places the vmcnt wait before the use)
+template <int AUX = 0>
 __device__ __forceinline__ v4u pg_load16(rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
+}
+__device__ __forceinline__ v4u pg_load16(rsrc_t r, uint32_t voff, uint32_t soff, int aux) {
+  return aux == 2 ? pg_load16<2>(r, voff, soff) : pg_load16<0>(r, voff, soff);
 }
 
 struct PgEpi {
@@ -508,7 +518,8 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   auto res_issue = [&](const Src& s, auto I) __attribute__((always_inline)) {
     constexpr int i = decltype(I)::value;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) resv[i % 3][k] = pg_load16(r_res, res_off(s, i, k), 0u);
+    for (int k = 0; k < 4; ++k)
+      resv[i % 3][k] = pg_load16(r_res, res_off(s, i, k), 0u, NQK_PG_RLAUX >= 0 ? NQK_PG_RLAUX : (NK == 48 ? 2 : 0));
   };
   auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
     const int8_t* cp = lds + PG_COLP + cslot * 2048;

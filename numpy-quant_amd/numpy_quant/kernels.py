@@ -336,9 +336,46 @@ def openblas_threads() -> int:
 def gemv_t_applies(M: int, N: int, K: int) -> bool:
     """NumPy sends a one-row product x[1, K] @ B[K, N] (N > 1) whose B has unit stride
     along K to OpenBLAS GEMV-T; nqk_sgemv_t reproduces its order for K >= 9 and K = 1, 4
-    (pinned against np.matmul; K in 2..8 other than 4 takes special small-matrix paths
-    there that are not restated)."""
+    (pinned against np.matmul; K in 2..8 other than 4 take OpenBLAS's small-m kernels:
+    small_one_row / nqk_sgemv_small)."""
     return M == 1 and N > 1 and (K >= 9 or K in (1, 4))
+
+
+def small_one_row(N: int, K: int) -> bool:
+    """One-row products NumPy does not send to the GEMV-T kernels that nqk_sgemv_t restates:
+    a 1 x 1 result (cblas_sdot) and K in 2..8 except 4 (OpenBLAS's small-m GEMV-T kernels);
+    nqk_sgemv_small computes them."""
+    return N == 1 or (2 <= K <= 8 and K != 4)
+
+
+def one_row_restated(N: int, K: int) -> bool:
+    """Whether x[1, K] @ B[K, N] with B's columns contiguous (a Gemm's w.T) is computed in
+    NumPy's exact order (pinned against np.matmul, tests/test_host.py): sdot below 32 rows;
+    GEMV-T for K = 1, 4 and K >= 9; the small-m kernels for K = 2, 5 (every N), K = 6, 7
+    when N % 8 < 4 and K = 3 when N % 8 in (0, 2).  Elsewhere (sdot from 32 rows, the
+    4-column blocks of K = 3, 6, 7, K = 8) the result may differ by ulps."""
+    if N == 1:
+        return K < 32
+    if K in (2, 5):
+        return True
+    if K in (6, 7):
+        return N % 8 < 4
+    if K == 3:
+        return N % 8 in (0, 2)
+    if K == 8:
+        return False
+    return gemv_t_applies(1, N, K)
+
+
+def sgemv_small(x: DeviceArray, bt: DeviceArray) -> DeviceArray:
+    """y[1, N] = x[1, K] . bt[N, K]^T for small_one_row shapes (nqk_sgemv_small)."""
+    N, Kb = bt.shape
+    K = x.shape[-1]
+    if Kb != K or x.size != K:
+        raise ValueError(f"matmul: mismatch in core dimension ({K} vs {Kb})")
+    y = DeviceArray((1, N), np.float32)
+    _lib.call("nqk_sgemv_small", x.vp, bt.vp, y.vp, N, K, K)
+    return y
 
 
 def sgemv_t(x: DeviceArray, bt: DeviceArray) -> DeviceArray:
@@ -358,6 +395,9 @@ def matmul_f32(a: DeviceArray, b: DeviceArray) -> DeviceArray:
     K2, N = b.shape[-2:]
     if K != K2:
         raise ValueError(f"matmul: mismatch in core dimension ({K} vs {K2})")
+    if a.ndim == 2 and b.ndim == 2 and M == 1 and N == 1:
+        # a 1 x 1 result: NumPy's matmul calls cblas_sdot (nqk_sgemv_small)
+        return sgemv_small(a, b.reshape((1, K)))
     out_batch, bmap = batch_map(a.shape[:-2], b.shape[:-2])
     if bmap is None:
         a = materialize_broadcast(a, out_batch + (M, K))

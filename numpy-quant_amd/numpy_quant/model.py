@@ -99,10 +99,15 @@ def _gemm(inputs, attrs):
         x = x.T
     if attrs.get("transB"):
         if (isinstance(x, FTensor) and isinstance(w, FTensor) and x.dev.ndim == 2 and w.dev.ndim == 2
-                and K.gemv_t_applies(x.dev.shape[0], w.dev.shape[0], x.dev.shape[1])):
+                and x.dev.shape[0] == 1):
             # x[1, K] @ w.T: NumPy's matmul takes OpenBLAS GEMV-T for this layout (the
-            # w.T view has its columns contiguous), whose summation order differs from GEMM's
-            return [FTensor(K.sgemv_t(x.dev, w.dev)) + b]
+            # w.T view has its columns contiguous), or sdot for one column, whose summation
+            # orders differ from GEMM's
+            n, k = w.dev.shape
+            if K.small_one_row(n, k):
+                return [FTensor(K.sgemv_small(x.dev, w.dev)) + b]
+            if K.gemv_t_applies(1, n, k):
+                return [FTensor(K.sgemv_t(x.dev, w.dev)) + b]
         w = w.T
     return [x.matmul(w) + b]
 

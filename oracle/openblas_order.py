@@ -135,7 +135,10 @@ def _chunk(a, x, y):
         if (n - n4) & 2:
             y[n4:n4 + 2] = _f(y[n4:n4 + 2] + _k4x2(blk[:, n4:n4 + 2], xb))
         if (n - n4) & 1:
-            y[n - 1:n] = _f(y[n - 1:n] + _k4x1(blk[:, n - 1:n], xb))
+            if m == 4:  # K = 4: the single leftover column is one multiply-add chain
+                y[n - 1:n] = _f(y[n - 1:n] + _chain(xb, blk[:, n - 1:n].T, False))
+            else:
+                y[n - 1:n] = _f(y[n - 1:n] + _k4x1(blk[:, n - 1:n], xb))
         k0 += nb
     if m3:
         # K % 4 trailing rows in C with GCC's fma contraction: one row is
@@ -181,3 +184,60 @@ def sgemv_t(b_t: np.ndarray, x: np.ndarray, threads: int | None = None) -> np.nd
         _chunk(a[:, j0:j1], x, yc)
         y[j0:j1] = yc
     return y
+
+
+# --------------------------------------------------------------------------------------
+# The one-row products outside the GEMV-T kernels above, identified against np.matmul in
+# this container (tests/test_host.py::test_small_one_row_orders_match_numpy_matmul):
+#  * a 1 x 1 result goes to cblas_sdot: below 32 rows the f32 products are summed in double
+#    in order and the sum rounded once (sdot's scalar tail; from 32 rows a vector kernel
+#    whose order is not restated);
+#  * K in 2..8 except 4 goes to OpenBLAS's small-m GEMV-T kernels: columns in blocks of 16
+#    (K = 2), 4 (K = 5) or 8 (K = 3, 6, 7) are k-ordered fma chains, leftover columns
+#    multiply-add chains, except a leftover 4-column block (K = 3, 6, 7) and a last odd
+#    column (K = 3), and K = 8 altogether, whose orders are not restated;
+#  * K = 4: the GEMV-T kernels above, except a single leftover column (N odd), which is a
+#    multiply-add chain.
+
+
+def sdot(x: np.ndarray, w: np.ndarray) -> np.float32:
+    """x . w for a 1 x 1 matmul result (len < 32)."""
+    p = (np.asarray(x, np.float32) * np.asarray(w, np.float32)).astype(np.float32)
+    d = 0.0
+    for v in p:
+        d += float(v)
+    return np.float32(d)
+
+
+def _chain(x, w, fma: bool):
+    acc = np.zeros(w.shape[0], np.float32)
+    for k in range(w.shape[1]):
+        xk = np.broadcast_to(np.float32(x[k]), acc.shape)
+        acc = _fma(xk, w[:, k], acc) if fma else _f(acc + _mul(xk, w[:, k]))
+    return acc
+
+
+def small_modes(N: int, K: int) -> str:
+    """Per column: 'F' fma chain, 'M' multiply-add chain, '?' not restated (K in 2..8, not 4)."""
+    blk = 16 if K == 2 else (4 if K == 5 else 8)
+    f_end = N // blk * blk
+    if K == 8:
+        return "?" * N
+    tail = ""
+    r = N - f_end
+    if K in (3, 6, 7) and r >= 4:
+        tail, r = "????", r - 4
+    if K == 3:
+        tail += ("MM" if r & 2 else "") + ("?" if r & 1 else "")
+    else:
+        tail += "M" * r
+    return "F" * f_end + tail
+
+
+def sgemv_small(b_t: np.ndarray, x: np.ndarray) -> np.ndarray:
+    """y = b_t . x for K in 2..8 except 4 ('?' columns computed as fma chains)."""
+    b_t = np.asarray(b_t, np.float32)
+    x = np.asarray(x, np.float32)
+    modes = small_modes(*b_t.shape)
+    fm = np.array([m != "M" for m in modes])
+    return np.where(fm, _chain(x, b_t, True), _chain(x, b_t, False)).astype(np.float32)

@@ -289,6 +289,83 @@ def gen_vit_part(out_dir, fname, tag, batch, bit_widths=(8, 4), seed=0, keep_sma
     print("wrote", tag)
 
 
+def gen_api(out_dir):
+    """Reference API surfaces outside the node loops (VERDICT r2 missing #4 / next #8):
+    QTensor.sigmoid (tensor.py:217-221), QTensor.relu on narrow storage (tensor.py:212-215),
+    tensor_min_max / quantize_tensor_min_max (tensor.py:232-242); Model.quantize of the MLP
+    on ONE calibration sample (one-row float products: model.py:328-442) and of the full
+    ViT-Base graph on the bench's 8 calibration images (quantization parameters only)."""
+    rng = np.random.default_rng(20261017)
+    arrays, meta = {}, {}
+    # QTensor.sigmoid: int8 storage, several scales / zero points (incl. None)
+    sig = []
+    for i, (bw, s, zp) in enumerate([(8, 0.05, 3), (8, 0.0123, -20), (4, 0.3, 2), (8, 0.031, None), (6, 0.11, 0)]):
+        lo, hi = (-(1 << (bw - 1)), (1 << (bw - 1)) - 1)
+        q = rng.integers(lo, hi + 1, size=(7, 33), dtype=np.int64)
+        zpa = None if zp is None else (np.int64(0) if zp == 0 else np.array(zp, np.int64))
+        t = rt.QTensor(q, bw, np.array(s, np.float32), zpa)
+        y = t.sigmoid()
+        arrays[f"sig{i}_q"] = q
+        arrays[f"sig{i}_y"] = np.asarray(y.data, np.int64)
+        sig.append({"bw": bw, "scale": s, "zp": zp})
+    meta["sigmoid"] = sig
+    # QTensor.relu (int64 data, as the reference requires) with zero points inside / outside the storage range
+    rel = []
+    for i, zp in enumerate([5, -3, 140, -300]):
+        q = rng.integers(-128, 128, size=(9, 17), dtype=np.int64)
+        y = rt.QTensor(q, 8, np.array(0.02, np.float32), np.array(zp, np.int64)).relu()
+        arrays[f"relu{i}_q"] = q
+        arrays[f"relu{i}_y"] = np.asarray(y.data)
+        rel.append({"zp": zp, "dtype": str(np.asarray(y.data).dtype)})
+    meta["relu"] = rel
+    # tensor_min_max / quantize_tensor_min_max on FTensors of mixed / one-signed data
+    mm = []
+    for i, (shift, scale) in enumerate([(0.0, 1.0), (3.0, 0.5), (-4.0, 0.25), (0.0, 1e-3), (0.7, 2.0)]):
+        x = (rng.standard_normal((5, 41)) * scale + shift).astype(np.float32)
+        mn, mx = rt.tensor_min_max(rt.FTensor(x))
+        arrays[f"mm{i}_x"] = x
+        rec = {"min_bits": int(np.asarray(mn, np.float32).view(np.uint32)),
+               "max_bits": int(np.asarray(mx, np.float32).view(np.uint32)),
+               "min_dtype": str(np.asarray(mn).dtype), "max_dtype": str(np.asarray(mx).dtype), "q": {}}
+        for bw in (8, 4):
+            for asym in (True, False):
+                qt = rt.quantize_tensor_min_max(rt.FTensor(x), bw, asym)
+                key = f"{bw}_{int(asym)}"
+                arrays[f"mm{i}_q{key}"] = np.asarray(qt.data, np.int64)
+                rec["q"][key] = {"scale_bits": int(np.asarray(qt.scale, np.float32).view(np.uint32)),
+                                 "zp": None if qt.zero_point is None else int(qt.zero_point)}
+        mm.append(rec)
+    meta["minmax"] = mm
+    # the MLP calibrated on one sample (X[0:1]), run on the whole set, bit widths 8 and 4
+    from sklearn.datasets import make_circles
+    X, _ = make_circles(n_samples=100, noise=0.03, random_state=0)
+    X = X.astype(np.float32)
+    proto = onnx_proto.load(os.path.join(REF, "models", "mlp.onnx"))
+    one = {}
+    for i in (0, 7):
+        for bw in (8, 4):
+            model = reference_model(proto)
+            qmodel = model.quantize([X[i:i + 1]], bit_width=bw)
+            out = qmodel([X])[0]
+            arrays[f"mlp1_{i}_bw{bw}_out"] = out
+            one[f"{i}_bw{bw}"] = qparams_json(qmodel.quant_params)
+    meta["mlp_one_sample"] = one
+    # ViT-Base calibrated on the bench's 8 images (bench.py build_vit: seed 12345)
+    vproto = onnx_proto.load(os.path.join(REF, "models", "vit", "vit_image_classifier_no_weights.onnx"),
+                             synthetic_weights=True)
+    onnx_proto.rebatch(vproto, 8)
+    x_cal = np.random.default_rng(12345).standard_normal((8, 3, 224, 224)).astype(np.float32)
+    t0 = time.time()
+    vmodel = reference_model(vproto)
+    vq = vmodel.quantize([x_cal], bit_width=8)
+    meta["vit_b8_calibration"] = {"qparams": qparams_json(vq.quant_params), "seconds": time.time() - t0,
+                                  "seed": 12345}
+    np.savez_compressed(os.path.join(out_dir, "api.npz"), **arrays)
+    with open(os.path.join(out_dir, "api.json"), "w") as fh:
+        json.dump(meta, fh, indent=0, sort_keys=True)
+    print("wrote api fixtures")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--vit", action="store_true", help="also run the full ViT-Base graph (B=1, ~3 min)")
@@ -306,6 +383,8 @@ def main():
         gen_vit_part(HERE, "vit_image_classifier_self_attention_no_weights.onnx", "attn_b2", 2, bit_widths=(8,))
     if not only or "layer" in only:
         gen_vit_part(HERE, "vit_image_classifier_encoder_layer_no_weights.onnx", "layer_b1", 1, keep_small=False)
+    if not only or "api" in only:
+        gen_api(HERE)
     if args.vit or (only and "vit" in only):
         gen_vit_part(HERE, "vit_image_classifier_no_weights.onnx", "vit_b1", 1, bit_widths=(8,), keep_small=False)
 

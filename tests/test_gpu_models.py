@@ -94,11 +94,12 @@ def ref_qparams(meta_qp):
 
 def tainted_values(model):
     """Values downstream of a float one-row product (M = 1) whose OpenBLAS order is not
-    reproduced: a one-row Gemm against a transposed weight goes to OpenBLAS GEMV-T, which
-    nqk_sgemv_t reproduces (oracle/openblas_order.py; K >= 9); other one-row products
-    (GEMV-N, dot, tiny K) are not restated, so values downstream of them may differ by
-    ulps.  Every GEMM with M > 1, any K, is reproduced (OpenBLAS's GEMM_Q = 448 K blocks)."""
-    from numpy_quant.kernels import gemv_t_applies
+    reproduced: a one-row Gemm against a transposed weight goes to OpenBLAS GEMV-T (or its
+    small-m kernels, or sdot for one column), which nqk_sgemv_t / nqk_sgemv_small reproduce
+    where kernels.one_row_restated says so (oracle/openblas_order.py); GEMV-N (a one-row
+    MatMul against a row-major weight) is not restated, so values downstream of it may
+    differ by ulps.  Every GEMM with M > 1, any K, is reproduced (OpenBLAS's GEMM_Q = 448 K blocks)."""
+    from numpy_quant.kernels import one_row_restated
     bad = set()
     for node in model.nodes:
         ins = [i.name for i in node.inputs]
@@ -106,9 +107,11 @@ def tainted_values(model):
             a = node.inputs[0].data
             w = node.inputs[1].data
             if a.dev.ndim >= 2 and a.dev.shape[-2] == 1:
-                covered = (node.op == "Gemm" and node.attrs.get("transB") and not node.attrs.get("transA")
-                           and a.dev.ndim == 2 and w.dev.ndim == 2
-                           and gemv_t_applies(1, w.dev.shape[0], a.dev.shape[1]))
+                gemm_t = (node.op == "Gemm" and node.attrs.get("transB") and not node.attrs.get("transA")
+                          and a.dev.ndim == 2 and w.dev.ndim == 2)
+                n = w.dev.shape[0] if gemm_t else w.dev.shape[-1]
+                covered = ((gemm_t and one_row_restated(w.dev.shape[0], a.dev.shape[1]))
+                           or (a.dev.ndim == 2 and w.dev.ndim == 2 and n == 1 and a.dev.shape[1] < 32))
                 if not covered:
                     bad.update(o.name for o in node.outputs)
         if any(i in bad for i in ins):

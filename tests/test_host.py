@@ -206,6 +206,44 @@ def test_sgemv_order_matches_numpy_matmul(K, N, threads):
     np.testing.assert_array_equal(sgemv_t(w, x, threads).view(np.int32), ref.view(np.int32))
 
 
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 31])
+def test_small_one_row_orders_match_numpy_matmul(K):
+    """The one-row products outside the GEMV-T restatement (oracle/openblas_order.py
+    sdot / sgemv_small, K = 4's leftover column): every column the oracle calls restated
+    equals np.matmul bit for bit, for N = 1 (sdot) and N = 2..70; and
+    kernels.one_row_restated (what the product reports) says restated exactly where the
+    oracle has no '?' column."""
+    threadpoolctl = pytest.importorskip("threadpoolctl")
+    info = [i for i in threadpoolctl.threadpool_info() if i.get("internal_api") == "openblas"]
+    if not info or info[0].get("architecture") not in ("Haswell", "Zen", "SkylakeX", "Cooperlake", "SapphireRapids"):
+        pytest.skip("OpenBLAS does not run its Haswell-family GEMV kernels on this host")
+    from oracle.openblas_order import sdot, sgemv_small, sgemv_t, small_modes
+    from numpy_quant.kernels import one_row_restated, small_one_row
+    rng = np.random.default_rng(1000 + K)
+    for N in list(range(1, 41)) + [63, 70]:
+        for _ in range(6):
+            x = rng.standard_normal(K).astype(np.float32)
+            w = rng.standard_normal((N, K)).astype(np.float32)
+            ref = (x[None, :] @ w.T)[0]
+            if N == 1:
+                if K < 32:
+                    assert sdot(x, w[0]).view(np.int32) == ref.view(np.int32)[0], (K, N)
+                assert one_row_restated(N, K) == (K < 32)
+                continue
+            if small_one_row(N, K):
+                modes = small_modes(N, K)
+                got = sgemv_small(w, x)
+                ok = np.array([m != "?" for m in modes])
+                np.testing.assert_array_equal(got[ok].view(np.int32), ref[ok].view(np.int32), err_msg=f"K={K} N={N}")
+                assert one_row_restated(N, K) == bool(ok.all()), (K, N, modes)
+            else:
+                with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
+                    ref1 = (x[None, :] @ w.T)[0]
+                np.testing.assert_array_equal(sgemv_t(w, x, 1).view(np.int32), ref1.view(np.int32),
+                                              err_msg=f"K={K} N={N}")
+                assert one_row_restated(N, K)
+
+
 def test_redimension_vit_base_to_tiny():
     """onnx_proto.redimension (the metric's ViT-tiny from the reference's ViT-Base graph):
     every width-768 / MLP-3072 initializer dimension and the head / width Reshape
