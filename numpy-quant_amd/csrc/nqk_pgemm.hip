@@ -67,6 +67,14 @@ enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fus
 #define NQK_PG_RLAUX -1  // cache-policy bits of the RESID epilogue's residual loads: -1 = nt for K = 3072
                          // (FFN-down 144 -> 138 us) and plain for K = 768 (nt: out-proj 59 -> 70 us)
 #endif
+#ifndef NQK_PG_BREG
+#define NQK_PG_BREG 0  // 1: B fragments straight from L2 into VGPRs (buffer_load_dwordx4, one step ahead;
+                       // parity-tested, measured no faster: profiles/r03h_pg_breg_dropped.txt)
+                       // instead of LDS-DMA + ds_read (the wave's 64 weight columns are its own)
+#endif
+#ifndef NQK_PG_PAIR_DEFAULT
+#define NQK_PG_PAIR_DEFAULT 0  // k_pg as 512-thread two-half workgroups (NQK_PG_PAIR=0/1 at run time)
+#endif
 #ifndef NQK_PG_PRIO
 #define NQK_PG_PRIO 3  // 3: s_setprio 1 in the epilogue, 0 in the k loop (the epilogue's VALU ahead of the
                        // other workgroup's k loop on the SIMD: -2..-4 %, profiles/r03c_*); 1: the reverse;
@@ -270,29 +278,52 @@ __device__ __forceinline__ v2f gelu_fast2(v2f h) {
 constexpr float PG_QLIM = 0x1.fffffcp-2f;
 
 
-template <int EPI, int NK, bool F32X>
-__global__ void __launch_bounds__(256, 2)
+// PAIR: one 512-thread workgroup per CU made of two independent 4-wave halves (each with
+// its own 76 KiB of LDS and its own tile sequence) that share the k-loop barriers, so the
+// two waves of every SIMD run their k loops and their epilogues at the same time.  Two
+// separate workgroups drift into alternating phases, and then a SIMD runs one wave's
+// epilogue VALU alone at the single-wave issue rate (one instruction per 4 cycles) beside
+// an MFMA stream that does not overlap it (profiles/r03d_*: MFMA + GELU epilogue without
+// loads = the sum of the two); two waves in their epilogues together issue every 2 cycles.
+template <int EPI, int NK, bool F32X, bool PAIR>
+__global__ void __launch_bounds__(PAIR ? 512 : 256, PAIR ? 1 : 2)
 k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
      int stagger, PgEpi e) {
   static_assert(NK % PG_RD == 0 && NK >= 2 * PG_RD, "k_pg: NK a multiple of the ring depth");
   constexpr bool RESID = EPI == PG_RESID;
-  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  extern __shared__ __attribute__((aligned(16))) int8_t lds_all[];
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
+  const int wg_half = PAIR ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
+  int8_t* const lds = lds_all + wg_half * PG_LDS;
   const int l15 = lane & 15, lg = lane >> 4;
 
   // tiles: the workgroups with blockIdx % 8 == x (one XCD under round-robin placement)
   // walk the band [lo, hi) of tile ids, every nx-th tile from lo + jx; tile ids are
-  // row-panel major, so the tiles in flight on an XCD share A row panels in its L2
-  const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X, jx = blockIdx.x / X;
-  const int nx = (G - x + X - 1) / X;
+  // row-panel major, so the tiles in flight on an XCD share A row panels in its L2.
+  // PAIR: the halves are virtual workgroups 2 j and 2 j + 1 of the same XCD.
+  const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X;
+  const int nx = (PAIR ? 2 : 1) * ((G - x + X - 1) / X);
+  const int jx0 = (PAIR ? 2 : 1) * (blockIdx.x / X);
   const int lo = (int)((int64_t)ntiles * x / X), hi = (int)((int64_t)ntiles * (x + 1) / X);
-  const int first = lo + jx;
-  if (first >= hi) return;
-  const int cnt = (hi - first + nx - 1) / nx;
+  auto count_of = [&](int f) { return f < hi ? (hi - f + nx - 1) / nx : 0; };
+  int first = lo + jx0 + wg_half;
+  int cnt = count_of(first);
+  int iters = cnt;
+  if constexpr (PAIR) {
+    // both halves run the longer half's count (same barriers); a shorter half repeats its
+    // last tile, a half without tiles recomputes the other's (identical values rewritten)
+    iters = count_of(lo + jx0);
+    if (cnt == 0) {
+      first = lo + jx0;
+      cnt = iters;
+    }
+  }
+  if (iters == 0) return;
+  auto tile_at = [&](int it) { return first + (it < cnt ? it : cnt - 1) * nx; };
   // the second workgroup of a CU (under round-robin placement: blockIdx >= G / 2) starts
   // about half a tile later, so that the two workgroups' epilogues do not coincide
-  if (stagger > 0 && (int)blockIdx.x >= G / 2)
+  if (!PAIR && stagger > 0 && (int)blockIdx.x >= G / 2)
     for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(8);  // ~512 cycles each
 
   constexpr int64_t BSTRIDE = (int64_t)NK * PG_BN * PG_BK;  // bytes of one column panel
@@ -319,11 +350,15 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   auto issue_stage = [&](const Src& s, int kt, int slot) __attribute__((always_inline)) {
     if constexpr ((NQK_PG_DIAG & 4) != 0) return;
     int8_t* st = lds + slot * PG_STG;
-    pg_dma16(r_a, st + (2 * wave) * 1024, va, s.sa + kt * PG_BK);
-    pg_dma16(r_a, st + (2 * wave + 1) * 1024, va, s.sa + 16u * (uint32_t)lda + kt * PG_BK);
+    if constexpr ((NQK_PG_DIAG & 256) == 0) {  // (diagnostic 256: no A pieces, 128: no B pieces)
+      pg_dma16(r_a, st + (2 * wave) * 1024, va, s.sa + kt * PG_BK);
+      pg_dma16(r_a, st + (2 * wave + 1) * 1024, va, s.sa + 16u * (uint32_t)lda + kt * PG_BK);
+    }
+    if constexpr ((NQK_PG_DIAG & 128) == 0 && !NQK_PG_BREG) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
-      pg_dma16(r_b, st + PG_ASTG + (4 * wave + p) * 1024, vb, s.sb + (uint32_t)(kt * (PG_BN * PG_BK) + p * 1024));
+      for (int p = 0; p < 4; ++p)
+        pg_dma16(r_b, st + PG_ASTG + (4 * wave + p) * 1024, vb, s.sb + (uint32_t)(kt * (PG_BN * PG_BK) + p * 1024));
+    }
   };
   // column constants of a tile (ct[256] | bias[256], 2 KiB): wave w moves bytes
   // [512 w, 512 w + 512) with lanes 0..31 (one VMEM operation per wave, like every wave)
@@ -352,6 +387,17 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     if constexpr ((NQK_PG_DIAG & 16) != 0) return;
     constexpr int q = decltype(Q)::value;
     dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + PG_ASTG + q * 1024>(fb_base);
+  };
+  // BREG: the wave's B fragments of step kt straight into registers: subtile q of the stage
+  // image (the bytes LDS-DMA piece q would have written) at the offset the LDS fragment read
+  // would have used, so every instruction still reads one whole 1 KiB piece
+  const uint32_t vb2 = (uint32_t)(4096 * wave + 64 * l15 + 16 * (lg ^ pg_sw(l15)));
+  auto issue_b = [&](const Src& s, int kt, v4i (&dst)[4]) __attribute__((always_inline)) {
+    if constexpr (NQK_PG_BREG && (NQK_PG_DIAG & 4) == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        dst[q] = (v4i)pg_load16(r_b, vb2, s.sb + (uint32_t)(kt * (PG_BN * PG_BK) + q * 1024));
+    }
   };
   // 16 MFMAs of one half step (M-subtiles 4 h .. 4 h + 3) with fn(q) after MFMA q
   auto half = [&](auto H, auto FIRST, const v4i (&aa)[4], const v4i (&bb)[4], const v4i (&ci)[4], auto&& fn)
@@ -567,23 +613,28 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   // RESID: 8 x 4 stores after the stages (counted conservatively without the 6 x 4 residual
   // loads, which the compiler may hoist above the stage issues: a smaller count only waits more)
   constexpr int EOPS = RESID ? 32 : 8;
-  Src cur = src_of(first);
+  // BREG: per stage only the 2 A pieces are LDS-DMA (PWA); the B loads of step kt + 1 are
+  // issued in step kt (before stage kt + 2's A pieces) and waited for by the compiler at
+  // their first use; the next tile's B of step 0 goes out before its A stages
+  constexpr int PWA = NQK_PG_BREG ? 2 : PG_PW;
+  Src cur = src_of(tile_at(0));
   issue_colp(cur.tn, 0);
+  issue_b(cur, 0, b0);
   issue_stage(cur, 0, 0);
   issue_stage(cur, 1, 1);
   if constexpr (NQK_PG_PRIO == 2) {
     if ((int)blockIdx.x >= G / 2) __builtin_amdgcn_s_setprio(1);
   }
-  for (int it = 0; it < cnt; ++it) {
+  for (int it = 0; it < iters; ++it) {
     if constexpr (NQK_PG_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(0);
-    const bool more = it + 1 < cnt;
-    const Src nxt = src_of(first + (more ? it + 1 : it) * nx);
+    const bool more = it + 1 < iters;
+    const Src nxt = src_of(tile_at(more ? it + 1 : it));
     const int cs = it & 1;
     // stage 0 and this tile's column constants landed (younger: stage 1, the previous
     // epilogue's operations)
-    if (it == 0) pg_vmcnt<PG_PW>();
-    else pg_vmcnt<PG_PW + EOPS>();
+    if (it == 0) pg_vmcnt<PWA>();
+    else pg_vmcnt<PWA + EOPS>();
     if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     // initial accumulators: minus the zero-point column terms of the lane's 16 columns
@@ -593,9 +644,10 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       cinit[j] = pg_lds16(lds + PG_COLP + cs * 2048 + (64 * wave + (RESID ? 16 * j + 4 * lg : 16 * lg + 4 * j)) * 4);
     sfor<0, 4>([&](auto Q) __attribute__((always_inline)) {
       rd_a(a_lo, ic<0>{}, ic<0>{}, Q);
-      rd_b(b0, ic<0>{}, Q);
+      if constexpr (!NQK_PG_BREG) rd_b(b0, ic<0>{}, Q);
     });
-    pg_lgkm_tie8(a_lo, b0);
+    if constexpr (NQK_PG_BREG) pg_lgkm_tie(a_lo[0], a_lo[1], a_lo[2], a_lo[3]);
+    else pg_lgkm_tie8(a_lo, b0);
     pg_lgkm_tie(cinit[0], cinit[1], cinit[2], cinit[3]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) cinit[j] = -cinit[j];
@@ -604,19 +656,23 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       constexpr int slot = kt % PG_RD;
       v4i(&bc)[4] = (kt & 1) ? b1 : b0;
       v4i(&bn)[4] = (kt & 1) ? b0 : b1;
-      if constexpr (kt > 0) pg_lgkm_tie8(a_lo, bc);  // this step's fragments (read in step kt - 1)
+      if constexpr (kt > 0) {  // this step's fragments (read in step kt - 1)
+        if constexpr (NQK_PG_BREG) pg_lgkm_tie(a_lo[0], a_lo[1], a_lo[2], a_lo[3]);
+        else pg_lgkm_tie8(a_lo, bc);
+      }
       // first half: subtiles 0..3; between the MFMAs the second half's A fragments and the
       // refill of the slot step kt - 1 read (stage kt + 2)
       half(ic<0>{}, std::integral_constant<bool, kt == 0>{}, a_lo, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
         constexpr int q = decltype(Q)::value;
         if constexpr (q < 4) rd_a(a_hi, ic<slot>{}, ic<4>{}, Q);
+        if constexpr (q == 2 && NQK_PG_BREG && kt + 1 < NK) issue_b(cur, kt + 1, bn);
         if constexpr (q == 4 && kt + 2 < NK) issue_stage(cur, kt + 2, (kt + 2) % PG_RD);
       });
       if constexpr (kt == 1) issue_colp(nxt.tn, cs ^ 1);
       if constexpr (kt + 1 < NK) {
         // stage kt + 1 landed; younger: stage kt + 2 (if issued), colp (step 1), and for
         // stage 1 the previous tile's epilogue operations
-        constexpr int y = (kt + 2 < NK ? PG_PW : 0) + ((kt == 1 || kt == 2) ? 1 : 0);
+        constexpr int y = (kt + 2 < NK ? PWA : 0) + ((kt == 1 || kt == 2) ? 1 : 0) + (NQK_PG_BREG ? 4 : 0);
         if (kt == 0 && it > 0) pg_vmcnt<y + EOPS>();
         else pg_vmcnt<y>();
         pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
@@ -629,7 +685,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         constexpr int q = decltype(Q)::value;
         if constexpr (kt + 1 < NK) {
           if constexpr (q < 4) rd_a(a_lo, ic<(kt + 1) % PG_RD>{}, ic<0>{}, Q);
-          else if constexpr (q < 8) rd_b(bn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
+          else if constexpr (q < 8 && !NQK_PG_BREG) rd_b(bn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
         }
       });
     });
@@ -643,6 +699,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     }
     // (the last tile re-stages its own first stages: never read, drained at the end; the
     // VMEM counts stay the same on every path)
+    issue_b(nxt, 0, b0);
     issue_stage(nxt, 0, 0);
     issue_stage(nxt, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
@@ -1217,16 +1274,23 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   // initial delay of the second workgroup per CU, in units of s_sleep 8 (~512 cycles)
   const char* sv = getenv("NQK_PG_STAGGER");
   const int stg = grid == slots ? (sv ? atoi(sv) : 0) : 0;
-  const int key = epi * 4 + (K == 3072 ? 2 : 0) + (f32x ? 1 : 0);
+  const char* pv = getenv("NQK_PG_PAIR");
+  const bool pair = pv ? atoi(pv) != 0 : NQK_PG_PAIR_DEFAULT;
+  const int key = epi * 8 + (K == 3072 ? 2 : 0) + (f32x ? 1 : 0) + (pair ? 4 : 0);
   switch (key) {
-#define PGL(E, NKV, X)                                                                                          \
-  case E * 4 + (NKV == 48 ? 2 : 0) + (X ? 1 : 0):                                                               \
-    hipLaunchKernelGGL((k_pg<E, NKV, X>), dim3(grid), dim3(256), PG_LDS, stream(), a, bp, (int)M, (int)N, (int)lda, \
-                       tiles_n, nt, stg, e);                                                                    \
+#define PGL(E, NKV, X, P)                                                                                       \
+  case E * 8 + (NKV == 48 ? 2 : 0) + (X ? 1 : 0) + (P ? 4 : 0):                                                  \
+    hipLaunchKernelGGL((k_pg<E, NKV, X, P>), dim3(P ? (grid + 1) / 2 : grid), dim3(P ? 512 : 256),            \
+                       P ? 2 * PG_LDS : PG_LDS, stream(), a, bp, (int)M, (int)N, (int)lda, tiles_n, nt, stg, e); \
     break;
-    PGL(PG_QKV, 12, true)
-    PGL(PG_GELU, 12, true)
-    PGL(PG_RESID, 12, true) PGL(PG_RESID, 12, false) PGL(PG_RESID, 48, true) PGL(PG_RESID, 48, false)
+    PGL(PG_QKV, 12, true, false)
+    PGL(PG_GELU, 12, true, false)
+    PGL(PG_RESID, 12, true, false) PGL(PG_RESID, 12, false, false) PGL(PG_RESID, 48, true, false)
+    PGL(PG_RESID, 48, false, false)
+    PGL(PG_QKV, 12, true, true)
+    PGL(PG_GELU, 12, true, true)
+    PGL(PG_RESID, 12, true, true) PGL(PG_RESID, 12, false, true) PGL(PG_RESID, 48, true, true)
+    PGL(PG_RESID, 48, false, true)
 #undef PGL
     default:
       return 0;
