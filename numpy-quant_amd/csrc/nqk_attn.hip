@@ -141,7 +141,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   for (int idx = tid; idx < TP * 4; idx += 256) {
     const int row = idx >> 2, ch = idx & 3;
     const v4i z = {0, 0, 0, 0};
-    const v4i kv = row < T ? *reinterpret_cast<const v4i*>(k + row * 64 + ch * 16) : z;
+    // (diagnostic 64: no K loads)
+    const v4i kv = (row < T && (NQK_ATTN_DIAG & 64) == 0) ? *reinterpret_cast<const v4i*>(k + row * 64 + ch * 16) : z;
     *reinterpret_cast<v4i*>(Ks + swz64a(row, ch)) = kv;
   }
   // V^T by blocks of 4 tokens x 16 dims: four 16-B row loads, a 4 x 4 byte transpose per
@@ -153,7 +154,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tok = 4 * rb + r;
-      w[r] = tok < T ? *reinterpret_cast<const v4i*>(v + tok * 64 + c * 16) : v4i{0, 0, 0, 0};
+      w[r] = (tok < T && (NQK_ATTN_DIAG & 64) == 0) ? *reinterpret_cast<const v4i*>(v + tok * 64 + c * 16)
+                                                      : v4i{0, 0, 0, 0};
     }
 #if NQK_ATTN_DIAG & 1  // diagnostic builds only (wrong results): 1 = V^T staging skipped, 2 = exp
                       // replaced by one add, 4 = P quantize replaced by a convert
@@ -230,7 +232,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         for (int j = 0; j < 4; ++j) acc[4 * qq + j] = -(rowterm + ck[j]);
       }
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < 2 && (NQK_ATTN_DIAG & 8) == 0; ++s) {  // (diagnostic 8: no score MFMAs)
         const v4i ka = *reinterpret_cast<const v4i*>(Ks + swz64a(c * 32 + r32, 2 * s + h));
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(ka, qb[s], acc, 0, 0, 0);
       }
@@ -465,7 +467,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const v4i va = *reinterpret_cast<const v4i*>(Vt + vt_row(j * 32 + r32) + (2 * c + h) * 16);
-        acc2[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(va, pb, acc2[j], 0, 0, 0);
+        if constexpr ((NQK_ATTN_DIAG & 32) != 0) acc2[j][c] ^= va[0] ^ pb[j];  // (diagnostic 32: no PV MFMAs)
+        else acc2[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(va, pb, acc2[j], 0, 0, 0);
       }
     }
     rp += xor32i(rp);
@@ -486,7 +489,10 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           const int vv = acc2[j][4 * qq + jj] - rowp - cv[jj];
           o[jj] = FAST ? (float)vv * a.s_pv : (float)((double)vv * (double)a.s_pv);
         }
-        if constexpr (FAST) {
+        if constexpr ((NQK_ATTN_DIAG & 16) != 0) {  // (diagnostic 16: context bytes without the quantize)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) qs[jj] = (int)o[jj];
+        } else if constexpr (FAST) {
           bool sl[4];
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) qs[jj] = quant_filter(o[jj] * a.rs_ctx_f, a.zp_ctx_f, a.lo_f, a.hi_f, &sl[jj]);

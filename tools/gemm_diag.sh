@@ -13,7 +13,7 @@ mkdir -p build/diag ../../tools/diag
 for arg in "$@"; do
   name="${arg%%=*}"; flags="${arg#*=}"
   /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wno-unused-function \
-    -Wno-unused-variable --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt \
+    -Wno-unused-variable --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize \
     $flags -c ${SRC:-nqk_fused}.hip -o build/diag/${SRC:-nqk_fused}_$name.o
   objs=$(ls build/*.o | grep -v ${SRC:-nqk_fused}.o)
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/diag/libnqk_$name.so $objs \
