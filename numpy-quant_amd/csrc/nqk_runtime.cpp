@@ -12,7 +12,7 @@ hipStream_t g_streams[64] = {};
 constexpr int kSide = 3;           // side streams 1..3 (nqk_set_stream)
 hipStream_t g_side[64][kSide] = {};
 int g_cur = 0;                     // current stream index of the (single) host thread
-hipEvent_t g_fork = nullptr, g_join[kSide] = {};
+hipEvent_t g_fork[64] = {}, g_join[64][kSide] = {};  // per device, with that device's side streams
 hipEvent_t g_t0 = nullptr, g_t1 = nullptr;
 hipGraph_t g_capturing = nullptr;
 std::mutex g_mu;
@@ -88,9 +88,12 @@ static int ensure_side() {
     if (!g_side[g_device][i] &&
         check(hipStreamCreateWithFlags(&g_side[g_device][i], hipStreamNonBlocking), "hipStreamCreate"))
       return -1;
-    if (!g_join[i] && check(hipEventCreateWithFlags(&g_join[i], hipEventDisableTiming), "hipEventCreate")) return -1;
+    if (!g_join[g_device][i] &&
+        check(hipEventCreateWithFlags(&g_join[g_device][i], hipEventDisableTiming), "hipEventCreate"))
+      return -1;
   }
-  if (!g_fork && check(hipEventCreateWithFlags(&g_fork, hipEventDisableTiming), "hipEventCreate")) return -1;
+  if (!g_fork[g_device] && check(hipEventCreateWithFlags(&g_fork[g_device], hipEventDisableTiming), "hipEventCreate"))
+    return -1;
   return 0;
 }
 
@@ -103,17 +106,17 @@ int nqk_set_stream(int which) {
 
 int nqk_stream_fork(void) {
   if (ensure_side()) return -1;
-  if (check(hipEventRecord(g_fork, g_streams[g_device]), "hipEventRecord")) return -1;
+  if (check(hipEventRecord(g_fork[g_device], g_streams[g_device]), "hipEventRecord")) return -1;
   for (int i = 0; i < kSide; ++i)
-    if (check(hipStreamWaitEvent(g_side[g_device][i], g_fork, 0), "hipStreamWaitEvent")) return -1;
+    if (check(hipStreamWaitEvent(g_side[g_device][i], g_fork[g_device], 0), "hipStreamWaitEvent")) return -1;
   return 0;
 }
 
 int nqk_stream_join(void) {
   if (ensure_side()) return -1;
   for (int i = 0; i < kSide; ++i) {
-    if (check(hipEventRecord(g_join[i], g_side[g_device][i]), "hipEventRecord")) return -1;
-    if (check(hipStreamWaitEvent(g_streams[g_device], g_join[i], 0), "hipStreamWaitEvent")) return -1;
+    if (check(hipEventRecord(g_join[g_device][i], g_side[g_device][i]), "hipEventRecord")) return -1;
+    if (check(hipStreamWaitEvent(g_streams[g_device], g_join[g_device][i], 0), "hipStreamWaitEvent")) return -1;
   }
   return 0;
 }
@@ -150,9 +153,9 @@ int nqk_graph_abort(void) {
   // capture after a fork), end the capture and drop the partial graph
   g_cur = 0;
   for (int i = 0; g_device >= 0 && i < kSide; ++i)
-    if (g_side[g_device][i] && g_join[i]) {
-      (void)hipEventRecord(g_join[i], g_side[g_device][i]);
-      (void)hipStreamWaitEvent(g_streams[g_device], g_join[i], 0);
+    if (g_side[g_device][i] && g_join[g_device][i]) {
+      (void)hipEventRecord(g_join[g_device][i], g_side[g_device][i]);
+      (void)hipStreamWaitEvent(g_streams[g_device], g_join[g_device][i], 0);
     }
   hipGraph_t g = nullptr;
   (void)hipStreamEndCapture(stream(), &g);

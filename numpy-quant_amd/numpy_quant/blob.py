@@ -40,6 +40,11 @@ ALIGN = 256
 
 def _enc_qp(p) -> list:
     s = p.scale
+    # the header keeps the reference's exact types (np.float32 scalar or 0-d f32 array):
+    # anything else would come back narrowed to float32, a different Python object
+    if not ((isinstance(s, np.floating) and s.dtype == np.float32) or
+            (isinstance(s, np.ndarray) and s.dtype == np.float32 and s.ndim == 0)):
+        raise ValueError(f"blob: scale {s!r} ({type(s).__name__}) is not a float32 scalar")
     skind = 0 if isinstance(s, np.floating) else 1
     bits = int(np.asarray(s, dtype=np.float32).view(np.uint32))
     z = p.zero_point

@@ -329,6 +329,21 @@ class Model:
         those constants are taken as they are instead of being quantized here."""
         constants = constants or {}
         wanted = {}
+        if constants:
+            # a blob must carry exactly this graph's constants, each with this graph's shape:
+            # never quietly re-quantize a missing one from local weights, never attach a
+            # blob of another model whose initializer names happen to match
+            graph_consts = {v.name: v for v in self.values if isinstance(v, Constant)}
+            missing = sorted(set(graph_consts) - set(constants))
+            extra = sorted(set(constants) - set(graph_consts))
+            if missing or extra:
+                raise ValueError(f"blob constants differ from the graph's: missing {missing[:5]}, "
+                                 f"unknown {extra[:5]}")
+            for name, t in constants.items():
+                d = graph_consts[name].data
+                want = None if d is None else tuple(d.dev.shape if hasattr(d, "dev") else np.shape(d.data))
+                if want is not None and tuple(t.dev.shape) != want:
+                    raise ValueError(f"blob constant {name}: shape {tuple(t.dev.shape)}, graph {want}")
 
         def qconst(value, bw, scale, zp):
             t = constants.get(value.name)

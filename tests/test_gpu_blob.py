@@ -56,6 +56,30 @@ def test_vit_blob_round_trip(tmp_path):
     np.testing.assert_array_equal(q2([x])[0], want)
 
 
+def test_blob_of_another_graph_is_refused(tmp_path):
+    """A blob attaches only to a graph with exactly its constants and shapes:
+    the ViT-Ti blob (redimensioned graph, same initializer names) must not attach to the
+    ViT-Base graph, and the MLP blob not to the ViT."""
+    from numpy_quant import onnx_proto
+    from numpy_quant.model import Model
+    path_onnx = os.path.join(MODELS, "vit_image_classifier_no_weights.onnx")
+    tiny = onnx_proto.load(path_onnx, synthetic_weights=True)
+    onnx_proto.redimension(tiny, 192, 3, 768)
+    x = np.random.default_rng(5).standard_normal((1, 3, 224, 224)).astype(np.float32)
+    qtiny = Model.from_onnx(tiny).quantize([x], bit_width=8)
+    blob = tmp_path / "tiny.nqk"
+    qtiny.save(blob)
+    base = Model.from_onnx(onnx_proto.load(path_onnx, synthetic_weights=True))
+    with pytest.raises(ValueError, match="shape"):
+        base.load_quantized(blob)
+    X = np.load(os.path.join(GOLDEN, "mlp.npz"))["X"]
+    qmlp = Model.from_onnx(os.path.join(MODELS, "mlp.onnx")).quantize([X], bit_width=8)
+    mblob = tmp_path / "mlp.nqk"
+    qmlp.save(mblob)
+    with pytest.raises(ValueError, match="differ"):
+        Model.from_onnx(onnx_proto.load(path_onnx, synthetic_weights=True)).load_quantized(mblob)
+
+
 def test_qtensor_relu_device():
     """tensor.py:212-215: values below the zero point become the zero point; a zero
     point outside the int8 storage range widens the storage."""

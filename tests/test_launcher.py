@@ -71,6 +71,11 @@ def test_blob_qparams_and_framing(tmp_path):
         assert type(q.zero_point) is type(p.zero_point)
         if p.zero_point is not None:
             assert int(q.zero_point) == int(p.zero_point)
+    # the header keeps the reference's exact scale types: a float64 or Python float scale is
+    # refused instead of being narrowed to float32 on the way
+    for bad in (np.float64(0.5), 0.5, np.array(0.5)):
+        with pytest.raises(ValueError):
+            blob._enc_qp(QuantizationParams(bad, None))
     header = {"version": 1, "bit_width": 8, "qparams": {}, "constants": [], "payload_bytes": 512}
     hb = blob.encode_header(header)
     head = blob.MAGIC + struct.pack("<Q", len(hb)) + hb
@@ -85,3 +90,26 @@ def test_blob_qparams_and_framing(tmp_path):
     path.write_bytes(b"NOTABLOB" + head[8:])
     with pytest.raises(ValueError):
         blob.read(path)
+
+
+def test_openblas_thread_resolution(monkeypatch):
+    """kernels.openblas_threads (the thread count whose GEMV-T column split the one-row
+    float products reproduce) reads what OpenBLAS reads: NQK_BLAS_THREADS, then
+    OPENBLAS_NUM_THREADS, GOTO_NUM_THREADS, OMP_NUM_THREADS, else the CPU affinity; at most
+    64 (the conftest fixture that pins 8 for the other tests is bypassed here)."""
+    import os
+    from numpy_quant import kernels
+    monkeypatch.setattr(kernels, "BLAS_THREADS", None)
+    for v in ("NQK_BLAS_THREADS", "OPENBLAS_NUM_THREADS", "GOTO_NUM_THREADS", "OMP_NUM_THREADS"):
+        monkeypatch.delenv(v, raising=False)
+    assert kernels.openblas_threads() == max(1, min(len(os.sched_getaffinity(0)), 64))
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert kernels.openblas_threads() == 3
+    monkeypatch.setenv("GOTO_NUM_THREADS", "5")
+    assert kernels.openblas_threads() == 5
+    monkeypatch.setenv("OPENBLAS_NUM_THREADS", "200")
+    assert kernels.openblas_threads() == 64
+    monkeypatch.setenv("NQK_BLAS_THREADS", "2")
+    assert kernels.openblas_threads() == 2
+    monkeypatch.setenv("NQK_BLAS_THREADS", "x")
+    assert kernels.openblas_threads() == 64
