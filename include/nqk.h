@@ -177,6 +177,16 @@ int nqk_sgemm_embed(const float* cols, const float* w, const float* bias, const 
  * cols[(b,oy,ox)][(ki,kj,ci)] = f32((q[b][ci][oy*kh+ki][ox*kw+kj] - zp) * scale). */
 int nqk_patchify_dequant(const int8_t* q, float* cols, int64_t n, int64_t c, int64_t h, int64_t w, int64_t kh,
                          int64_t kw, float scale, int64_t zp);
+/* The patch embedding of a quantized image without the im2col matrix (round 3): the
+ * patchify + dequantize above folded into the A-operand load of the nqk_sgemm_embed GEMM,
+ * same bits (model.py:95-100 Conv on the dequantized input, tensor.py:256-264 fconv2d,
+ * numpy_helper.py:18-92 im2col, then the Reshape / Transpose / Concat / Add(pos) chain).
+ * q: int8 [images][3][h][w], 16 x 16 patches; wt: the weights as [N][768] in the
+ * (ki, kj, ci) order with every 16-block permuted to p = (k & 1) * 8 + (k >> 1)
+ * (numpy_quant/plan.py FusedEmbed); N % 64 == 0. */
+int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float* wt, const float* bias, const float* cls,
+                const float* pos, float* out, int64_t images, int64_t c, int64_t h, int64_t w, int64_t kh,
+                int64_t kw, int64_t N);
 int nqk_im2col(const float* x, float* cols, int64_t n, int64_t c, int64_t h, int64_t w,
                int64_t kh, int64_t kw, int64_t ph0, int64_t pw0, int64_t sh, int64_t sw,
                int64_t ho, int64_t wo);

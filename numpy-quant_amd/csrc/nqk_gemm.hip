@@ -397,6 +397,165 @@ k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __
     }
 }
 
+// Patch embedding with the patchify + dequantize folded into the A-operand load (round 3):
+// the quantized image (int8, NCHW, 3 channels, 16 x 16 patches) is read directly and the
+// dequantized im2col matrix never exists.  Same numerics as k_patchify_dequant +
+// k_sgemm_mfma<EMBED>: A[m][k] = f32((q - zp) * s) with k = (ki, kj, ci); each output a
+// k-ordered fmaf chain per BLAS K block (v_mfma_f32_32x32x2_f32 is one, tools/micro/f32mfma),
+// blocks summed in order, then bias and position embedding.  128 x (64 WN) tiles, 4 waves
+// (2 x 2), k-tiles of 16.  Operands sit in LDS as [row][16 k] with the k order permuted to
+// p = (k & 1) * 8 + (k >> 1) and 20-float rows, so a lane's 8 k values of one MFMA sub-tile
+// come in two conflict-free ds_read_b128 (k_sgemm_mfma: 32 ds_read_b32 per k-tile).  The
+// weights are pre-arranged once per plan as wt[N][K] in that order (plan.py FusedEmbed).
+// A: the thread of row r (tid & 127) and half hf (tid >> 7, wave-uniform) keeps the 3 channel
+// rows (3 x 16 B) of its patch for the current kernel row ki (3 k-tiles) in registers and
+// writes its 8 k values of each k-tile as two ds_write_b128.
+constexpr int EQ_ROW = 20;  // floats per LDS operand row (16 + 4 padding)
+template <int WN>
+__global__ void __launch_bounds__(256, 2)
+k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __restrict__ C, int64_t M, int64_t N,
+          int64_t hw, int64_t wo, int64_t H, int64_t W, float s, float zpf, KBlocks kb, EmbedEpi ee) {
+  typedef float v16f __attribute__((ext_vector_type(16)));
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  constexpr int BN = 64 * WN, K = 768;
+  __shared__ __attribute__((aligned(16))) float sa[2][128 * EQ_ROW];
+  __shared__ __attribute__((aligned(16))) float sb[2][BN * EQ_ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, r32 = lane & 31, h = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.y * 128, n0 = (int64_t)blockIdx.x * BN;
+  // A rows of this thread: patch m = image * hw + oy * wo + ox
+  const int ar = tid & 127, hf = tid >> 7;
+  const int64_t am = m0 + ar < M ? m0 + ar : M - 1;
+  const int64_t img = am / hw, pt = am - img * hw, oy = pt / wo, ox = pt - oy * wo;
+  const int8_t* qrow = q + ((img * 3) * H + oy * 16) * W + ox * 16;  // channel 0, kernel row 0
+  const int64_t cstride = H * W;
+  int4 px[3], pxn[3];
+  auto load_px = [&](int ki, int4 (&d)[3]) {
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci) d[ci] = *reinterpret_cast<const int4*>(qrow + ci * cstride + (int64_t)ki * W);
+  };
+  // B: thread t moves column cb = t >> 2 (and cb + 64 for WN = 2), k quarter t & 3
+  const int cb = tid >> 2, kq = tid & 3;
+  v4f bv[WN];
+  auto load_b = [&](int kt) {
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const int64_t n = n0 + cb + 64 * u;
+      bv[u] = n < N ? *reinterpret_cast<const v4f*>(wt + n * K + kt * 16 + 4 * kq) : v4f{0, 0, 0, 0};
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < WN; ++u) *reinterpret_cast<v4f*>(&sb[buf][(cb + 64 * u) * EQ_ROW + 4 * kq]) = bv[u];
+  };
+  // A values of k-tile sub (0..2 within kernel row): k_local = 8 hf + e -> j = 16 sub + k_local,
+  // kj = j / 3, ci = j % 3; written at p = (k_local & 1) * 8 + (k_local >> 1)
+  auto store_a = [&](int buf, auto SUB, const int4 (&d)[3]) __attribute__((always_inline)) {
+    constexpr int sub = decltype(SUB)::value;
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // both halves at compile-time offsets, the wave-uniform hf selects
+      const int j0 = 16 * sub + e, j1 = 16 * sub + 8 + e;
+      const int kj0 = j0 / 3, c0 = j0 % 3, kj1 = j1 / 3, c1 = j1 % 3;
+      const int w0 = (kj0 >> 2) == 0 ? d[c0].x : (kj0 >> 2) == 1 ? d[c0].y : (kj0 >> 2) == 2 ? d[c0].z : d[c0].w;
+      const int w1 = (kj1 >> 2) == 0 ? d[c1].x : (kj1 >> 2) == 1 ? d[c1].y : (kj1 >> 2) == 2 ? d[c1].z : d[c1].w;
+      const int qv = hf ? (int)(int8_t)(w1 >> (8 * (kj1 & 3))) : (int)(int8_t)(w0 >> (8 * (kj0 & 3)));
+      f[e] = ((float)qv - zpf) * s;
+    }
+    float* dst = &sa[buf][ar * EQ_ROW + 4 * hf];
+    *reinterpret_cast<v4f*>(dst) = v4f{f[0], f[2], f[4], f[6]};      // k_local even -> p = k_local / 2
+    *reinterpret_cast<v4f*>(dst + 8) = v4f{f[1], f[3], f[5], f[7]};  // odd -> 8 + k_local / 2
+  };
+  v16f acc[2][WN], tot[2][WN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = tot[i][j][r] = 0.0f;
+  int blk = 0;
+  int64_t bend = kb.n > 0 ? kb.end[0] : -1;
+  load_px(0, px);
+  load_b(0);
+  store_a(0, std::integral_constant<int, 0>{}, px);
+  store_b(0);
+  __syncthreads();
+  constexpr int NKT = K / 16;
+  // one k-tile; SUB = kt % 3 at compile time (the kernel row ki = kt / 3 in px)
+  auto step = [&](int kt, auto SUB) __attribute__((always_inline)) {
+    constexpr int sub = decltype(SUB)::value;
+    const int cur = kt & 1;
+    const bool more = kt + 1 < NKT;
+    if (more) {
+      load_b(kt + 1);
+      if constexpr (sub == 2) load_px((kt + 1) / 3, pxn);
+    }
+    v4f fa[2][2], fb[WN][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float* src = &sa[cur][(wm * 64 + i * 32 + r32) * EQ_ROW + 8 * h];
+      fa[i][0] = *reinterpret_cast<const v4f*>(src);
+      fa[i][1] = *reinterpret_cast<const v4f*>(src + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const float* src = &sb[cur][(wn * 32 * WN + j * 32 + r32) * EQ_ROW + 8 * h];
+      fb[j][0] = *reinterpret_cast<const v4f*>(src);
+      fb[j][1] = *reinterpret_cast<const v4f*>(src + 4);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][kk >> 2][kk & 3], fb[j][kk >> 2][kk & 3], acc[i][j], 0, 0, 0);
+    if ((int64_t)kt * 16 + 16 == bend) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            tot[i][j][r] = tot[i][j][r] + acc[i][j][r];
+            acc[i][j][r] = 0.0f;
+          }
+      ++blk;
+      bend = blk < kb.n ? kb.end[blk] : -1;
+    }
+    if (more) {
+      if constexpr (sub == 2) {
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) px[ci] = pxn[ci];
+      }
+      store_a(cur ^ 1, std::integral_constant<int, (sub + 1) % 3>{}, px);
+      store_b(cur ^ 1);
+    }
+    __syncthreads();
+  };
+  for (int ki = 0; ki < NKT / 3; ++ki) {
+    step(3 * ki, std::integral_constant<int, 0>{});
+    step(3 * ki + 1, std::integral_constant<int, 1>{});
+    step(3 * ki + 2, std::integral_constant<int, 2>{});
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int64_t gn = n0 + wn * 32 * WN + j * 32 + r32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (gm < M && gn < N) {
+          const uint32_t im = (uint32_t)gm / (uint32_t)ee.hw, t = (uint32_t)gm - im * (uint32_t)ee.hw;
+          const float y = tot[i][j][r] + ee.bias[gn];
+          C[((int64_t)im * (ee.hw + 1) + 1 + t) * N + gn] = y + ee.pos[(1 + (int64_t)t) * N + gn];
+        }
+      }
+    }
+}
+
 // class-token rows of the EMBED output: out[image][0][n] = cls[n] + pos[0][n]
 __global__ void k_embed_cls(const float* __restrict__ cls, const float* __restrict__ pos, float* __restrict__ out,
                             int64_t images, int64_t hw, int64_t n) {
@@ -726,6 +885,32 @@ extern "C" int nqk_sgemm_embed(const float* cols, const float* w, const float* b
   if (int rc = launch_status("nqk_sgemm_embed")) return rc;
   hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);
   return launch_status("nqk_sgemm_embed(cls)");
+}
+
+extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float* wt, const float* bias,
+                           const float* cls, const float* pos, float* out, int64_t images, int64_t c, int64_t h,
+                           int64_t w, int64_t kh, int64_t kw, int64_t N) {
+  if (images <= 0 || N <= 0) return 0;
+  if (c != 3 || kh != 16 || kw != 16 || h % 16 || w % 16)
+    return fail("nqk_embed_q: 3-channel images and 16 x 16 patches expected");
+  if (N % 64) return fail("nqk_embed_q: N % 64 == 0 expected");
+  if (zp < -(1 << 20) || zp > (1 << 20)) return fail("nqk_embed_q: zero point out of range");
+  if ((((uintptr_t)q) | ((uintptr_t)wt)) & 15) return fail("nqk_embed_q: unaligned operands");
+  const int64_t wo = w / 16, hw = (h / 16) * wo, M = images * hw, K = 768;
+  if ((M + 127) / 128 > 65535) return fail("nqk_embed_q: grid too large");
+  KBlocks kb;
+  if (blas_kblocks(K, &kb) || !kblocks_al16(K, kb)) return fail("nqk_embed_q: K blocking");
+  const float zpf = (float)zp;
+  if (N % 128 == 0) {
+    hipLaunchKernelGGL(k_embed_q<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
+                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw});
+  } else {
+    hipLaunchKernelGGL(k_embed_q<1>, dim3((unsigned)(N / 64), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
+                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw});
+  }
+  if (int rc = launch_status("nqk_embed_q")) return rc;
+  hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);
+  return launch_status("nqk_embed_q(cls)");
 }
 
 extern "C" int nqk_patchify_dequant(const int8_t* q, float* cols, int64_t n, int64_t c, int64_t h, int64_t w,

@@ -415,6 +415,13 @@ class FusedEmbed:
         if self.kk % 2 or self.bias.size != self.kout or self.cls.size != self.kout:
             raise NoMatch("embedding dimensions")
         self._cols = None
+        # nqk_embed_q (no im2col matrix): 3-channel 16 x 16 patches, N % 64 == 0; the
+        # weights as [N][K] in (ki, kj, ci) order, each 16-block of k permuted to
+        # p = (k & 1) * 8 + (k >> 1) (the kernel's LDS order)
+        self.wt = None
+        if (cin == 3 and m.kh == 16 and m.kw == 16 and self.kout % 64 == 0 and os.environ.get("NQK_EMBED_Q", "1") != "0"):
+            wt = permute(W, [0, 2, 3, 1]).reshape((self.kout, self.kk // 16, 8, 2))
+            self.wt = permute(wt, [0, 1, 3, 2]).reshape((self.kout, self.kk))
 
     def pre(self, qmodel):
         """at the Conv's position: the shape-only placeholder for the Shape consumer"""
@@ -439,7 +446,10 @@ class FusedEmbed:
         if eshape.size != 3 or int(eshape[0]) != n:
             raise ValueError(f"class-token Expand shape {eshape} does not match the batch {n}")
         out = DeviceArray((n, hw + 1, self.kout), np.float32)
-        if fused_in:
+        folded = fused_in and self.wt is not None and c == 3
+        if folded:
+            cols = None  # nqk_embed_q reads the int8 image itself
+        elif fused_in:
             # dequantize fused into the patch gather (the QTensor is read once, as int8); the
             # patch matrix stays with the step (two streams: see FusedLayer.run)
             if self._cols is None or self._cols.shape != (n * hw, self.kk):
@@ -451,6 +461,23 @@ class FusedEmbed:
             cols, ho, wo = KM.im2col(x.dev, m.kh, m.kw, (0, 0, 0, 0), (m.kh, m.kw))
             streams = _ONE_STREAM
         t0 = KM.TIMER.begin() if KM.TIMER is not None else None
+
+        if folded:
+            def part(s_idx, i0, nb):
+                qv = xd.dev.offset_view(i0 * c * h * w, (nb, c, h, w))
+                ov = out.offset_view(i0 * (hw + 1) * self.kout, (nb, hw + 1, self.kout))
+                _lib.call("nqk_embed_q", qv.vp, float(np.float32(xd.scale)), int(zp) if zp is not None else 0,
+                          self.wt.vp, self.bias.vp, self.cls.vp, self.posv.vp, ov.vp, nb, c, h, w, m.kh, m.kw,
+                          self.kout)
+
+            streams.halves(n, part)
+            if t0 is not None:
+                KM.TIMER.end("embed_sgemm", t0, (2 * n * hw * self.kk * self.kout,
+                                                 n * c * h * w + 4 * (self.kk * self.kout + n * (hw + 1) * self.kout)),
+                             unit="flop32")
+            m.add.outputs[0].data = FTensor(out)
+            m.conv_out.data = FusedAway(m.conv_out.name)
+            return
 
         def part(s_idx, i0, nb):
             cp = cols.offset_view(i0 * hw * self.kk, (nb * hw, self.kk))

@@ -89,6 +89,36 @@ def test_patchify_dequant_equals_dequantize_then_im2col(n, c, h, w, kh, kw, zp):
     np.testing.assert_array_equal(cols.to_host(), ref_cols.to_host())
 
 
+@pytest.mark.parametrize("n,h,w,N,zp", [(3, 224, 224, 768, -5), (2, 224, 224, 192, 0), (1, 32, 48, 64, 17),
+                                        (5, 64, 32, 128, -128)])
+def test_embed_q_equals_patchify_then_sgemm_embed(n, h, w, N, zp):
+    """nqk_embed_q (patchify + dequantize folded into the GEMM's A-operand load, round 3)
+    gives the bits of nqk_patchify_dequant + nqk_sgemm_embed (the im2col path, pinned to the
+    reference's fconv2d by test_gpu_kernels / vit_b1): bias, position embedding and the
+    class-token rows included; ragged last row tile (n * hw % 128 != 0) and N = 64 / 192."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray, permute
+    rng = np.random.default_rng(n * 1000 + N)
+    q = rng.integers(-128, 128, size=(n, 3, h, w), dtype=np.int8)
+    s = np.float32(0.0173)
+    W = (0.05 * rng.standard_normal((N, 3, 16, 16))).astype(np.float32)
+    hw = (h // 16) * (w // 16)
+    bias = DeviceArray.from_host((0.1 * rng.standard_normal(N)).astype(np.float32))
+    cls = DeviceArray.from_host(rng.standard_normal(N).astype(np.float32))
+    pos = DeviceArray.from_host(rng.standard_normal((hw + 1, N)).astype(np.float32))
+    Wd = DeviceArray.from_host(W)
+    wm = permute(Wd, [2, 3, 1, 0]).reshape((768, N))
+    cols = DeviceArray((n * hw, 768), np.float32)
+    qd = DeviceArray.from_host(q)
+    _lib.call("nqk_patchify_dequant", qd.vp, cols.vp, n, 3, h, w, 16, 16, float(s), zp)
+    ref = DeviceArray((n, hw + 1, N), np.float32)
+    _lib.call("nqk_sgemm_embed", cols.vp, wm.vp, bias.vp, cls.vp, pos.vp, ref.vp, n, hw, N, 768)
+    wt = permute(permute(Wd, [0, 2, 3, 1]).reshape((N, 48, 8, 2)), [0, 1, 3, 2]).reshape((N, 768))
+    out = DeviceArray((n, hw + 1, N), np.float32)
+    _lib.call("nqk_embed_q", qd.vp, float(s), zp, wt.vp, bias.vp, cls.vp, pos.vp, out.vp, n, 3, h, w, 16, 16, N)
+    np.testing.assert_array_equal(out.to_host().view(np.int32), ref.to_host().view(np.int32))
+
+
 _VARIANTS = [{}, {"NQK_GEMM_PP": "1"}, {"NQK_NO_F32X": "1"}, {"NQK_NO_F32X": "1", "NQK_GEMM_PP": "1"},
              {"NQK_NO_GELU_FILTER": "1", "NQK_NO_F32X": "1"}, {"PACK": "1"}, {"PACK": "1", "NQK_NO_F32X": "1"}]
 
