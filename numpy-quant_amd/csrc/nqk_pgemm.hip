@@ -63,6 +63,11 @@ enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fus
 #define NQK_PG_STAUX 2  // cache-policy bits of the epilogue's output stores: nt (profiles/r03c_*: out-proj
                         // 77 -> 60 us; 16 = sc1, the line leaves L2: no gain)
 #endif
+#ifndef NQK_PG_STAUX_RESID
+#define NQK_PG_STAUX_RESID 0  // the residual epilogues' f32 output stores: plain, so the LayerNorm that
+                              // reads the rows next finds them in the Infinity Cache (same-box bench A/B,
+                              // profiles/r03_store_policy_ab.txt: LN 46.4 -> 42.1 us, residual GEMMs equal)
+#endif
 #ifndef NQK_PG_RLAUX
 #define NQK_PG_RLAUX -1  // cache-policy bits of the RESID epilogue's residual loads: -1 = nt for K = 3072
                          // (FFN-down 144 -> 138 us) and plain for K = 768 (nt: out-proj 59 -> 70 us)
@@ -600,7 +605,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
           }
         }
         if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, res_off(s, i, k), 0, NQK_PG_STAUX);
+        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, res_off(s, i, k), 0, NQK_PG_STAUX_RESID);
       }
       if constexpr (i + 2 < 8) res_issue(s, ic<i + 2>{});
     });
