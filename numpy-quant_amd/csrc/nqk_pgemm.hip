@@ -294,7 +294,7 @@ template <int EPI, int NK, bool F32X, bool PAIR>
 __global__ void __launch_bounds__(PAIR ? 512 : 256, PAIR ? 1 : 2)
 k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
      int stagger, PgEpi e) {
-  static_assert(NK % PG_RD == 0 && NK >= 2 * PG_RD, "k_pg: NK a multiple of the ring depth");
+  static_assert(NK % PG_RD == 0 && (NK >= 2 * PG_RD || NK == PG_RD), "k_pg: NK a multiple of the ring depth");
   constexpr bool RESID = EPI == PG_RESID;
   extern __shared__ __attribute__((aligned(16))) int8_t lds_all[];
   const int lane = threadIdx.x & 63;
@@ -455,9 +455,12 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       const double zp = g3 == 0 ? e.zp_out[0] : (g3 == 1 ? e.zp_out[1] : e.zp_out[2]);
       void* op = g3 == 0 ? e.out[0] : (g3 == 1 ? e.out[1] : e.out[2]);
       // QKV: the head-layout buffer holds whole images, ceil(M / tokens) of them
+      // N % 256 != 0 (ViT-tiny): a wave whose 64 columns lie past N stores through a
+      // zero-size descriptor (dropped; its VMEM count stays that of every wave)
       const rsrc_t r_out = pg_rsrc(
-          op, (uint32_t)(EPI == PG_QKV ? (uint64_t)((M + e.tokens - 1) / e.tokens) * e.tokens * e.heads * e.hdim
-                                       : (uint64_t)M * e.ldo));
+          op, cw >= N ? 0u
+                      : (uint32_t)(EPI == PG_QKV ? (uint64_t)((M + e.tokens - 1) / e.tokens) * e.tokens * e.heads * e.hdim
+                                                 : (uint64_t)M * e.ldo));
       // QKV: u = v c1 + c2 with c2 = RN(bias rsf): within |v| k1 + kb of zp + 128 + t,
       // t = RN(RN(RN(v sacc) + bias) / s_out) (DESIGN.md §4.3 error bound); kb from the
       // lane's largest |c2|, folded into the lane's limit
@@ -559,6 +562,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   // are issued after subtile i's stores (0 and 1 before the next tile's stages); the
   // compiler places their waits (compiler-visible loads).
   const rsrc_t r_res = pg_rsrc(RESID ? e.resid : nullptr, RESID ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
+  const rsrc_t r_nul = pg_rsrc(RESID ? e.resid : nullptr, 0u);  // columns past N: loads return 0, stores drop
   constexpr int TR_ROW = 272;  // bytes per staged row (256 + 16: conflict-free b128 writes)
   int8_t* const tr = lds + 2 * PG_STG + wave * (16 * TR_ROW);
   const int ta = lane & 15, tb = lane >> 4;
@@ -570,14 +574,15 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     constexpr int i = decltype(I)::value;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      resv[i % 3][k] = pg_load16(r_res, res_off(s, i, k), 0u, NQK_PG_RLAUX >= 0 ? NQK_PG_RLAUX : (NK == 48 ? 2 : 0));
+      resv[i % 3][k] = pg_load16(s.tn * PG_BN + 64 * wave < N ? r_res : r_nul, res_off(s, i, k), 0u,
+                                 NQK_PG_RLAUX >= 0 ? NQK_PG_RLAUX : (NK == 48 ? 2 : 0));
   };
   auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
     const int8_t* cp = lds + PG_COLP + cslot * 2048;
     const v4i bb = pg_lds16(cp + 1024 + (64 * wave + 4 * ta) * 4);  // columns 4 a .. 4 a + 3
     const v2f b01 = v2f{__int_as_float(bb[0]), __int_as_float(bb[1])};
     const v2f b23 = v2f{__int_as_float(bb[2]), __int_as_float(bb[3])};
-    const rsrc_t r_out = pg_rsrc(e.out[0], (uint32_t)((uint64_t)M * e.ldo * 4));
+    const rsrc_t r_out = pg_rsrc(e.out[0], s.tn * PG_BN + 64 * wave < N ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
     const float sacc = e.sacc[0];
     sfor<0, 8>([&](auto I) __attribute__((always_inline)) {
       constexpr int i = decltype(I)::value;
@@ -1191,9 +1196,15 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   if (getenv("NQK_NO_PG")) return 0;
   if (bp == nullptr || p->colterm == nullptr || p->b_packed == 2) return 0;
   if (!(epi == PG_QKV || epi == PG_RESID || epi == PG_GELU)) return 0;
-  if (!(K == 768 || K == 3072) || N % PG_BN != 0 || M < PG_BM) return 0;
+  // K = 192 / 768 / 3072 (ViT-Ti / ViT-B widths and MLP), N % 64 == 0 (a partial last column
+  // tile: whole waves past N)
+  if (!(K == 192 || K == 768 || K == 3072) || N % 64 != 0 || M < PG_BM) return 0;
   if ((double)M * N * 4.0 >= 4294967295.0 || (double)M * lda >= 4294967295.0) return 0;
-  if ((epi == PG_QKV || epi == PG_GELU) && (!f32x || K != 768)) return 0;
+  if ((epi == PG_QKV || epi == PG_GELU) && (!f32x || K == 3072)) return 0;
+  // residual epilogues need whole 256-column tiles: at N = 192 (ViT-Ti) the 394 row-panel
+  // tiles of B = 256 fill 77 % of the slots with a quarter of each tile idle, and the
+  // one-tile-per-workgroup kernel is faster (29.1 vs 24.9 us, profiles/r03_vit_tiny_pg.txt)
+  if (epi == PG_RESID && N % PG_BN != 0) return 0;
   if (epi == PG_QKV && !(p->hdim == 64 && p->group_cols % 64 == 0 && (double)M * p->heads * p->hdim < 2147483647.0))
     return 0;
   // NQK_PG_NORESID=1 keeps the residual epilogues on k_qgemm_big (the round-2 kernel)
@@ -1249,13 +1260,13 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     const float g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
     e.g_lim = (float)((0.5 - (double)g_abs) * (1.0 - 0x1p-22));
   }
-  const int tiles_n = (int)(N / PG_BN), tiles_m = (int)((M + PG_BM - 1) / PG_BM);
+  const int tiles_n = (int)((N + PG_BN - 1) / PG_BN), tiles_m = (int)((M + PG_BM - 1) / PG_BM);
   const int nt = tiles_m * tiles_n;
   // k_pg (two workgroups per CU, epilogue after the k loop) by default; NQK_PG_KERNEL=2
   // selects k_pg2 (epilogue inside the next tile's k loop, one workgroup per CU), measured
   // slower (its interleaved epilogue does not hide behind the MFMAs)
   const char* kv = getenv("NQK_PG_KERNEL");
-  if (kv && atoi(kv) == 2) {
+  if (kv && atoi(kv) == 2 && K != 192 && N % PG_BN == 0) {
     const int grid2 = nt < pg_num_cus() ? nt : pg_num_cus();
     const int key2 = epi * 4 + (K == 3072 ? 2 : 0) + (f32x ? 1 : 0);
     switch (key2) {
@@ -1280,11 +1291,12 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   const char* sv = getenv("NQK_PG_STAGGER");
   const int stg = grid == slots ? (sv ? atoi(sv) : 0) : 0;
   const char* pv = getenv("NQK_PG_PAIR");
-  const bool pair = pv ? atoi(pv) != 0 : NQK_PG_PAIR_DEFAULT;
-  const int key = epi * 8 + (K == 3072 ? 2 : 0) + (f32x ? 1 : 0) + (pair ? 4 : 0);
+  const bool pair = K != 192 && (pv ? atoi(pv) != 0 : NQK_PG_PAIR_DEFAULT);
+  const int kc = K == 3072 ? 2 : (K == 192 ? 1 : 0);
+  const int key = epi * 16 + kc * 4 + (f32x ? 1 : 0) + (pair ? 2 : 0);
   switch (key) {
 #define PGL(E, NKV, X, P)                                                                                       \
-  case E * 8 + (NKV == 48 ? 2 : 0) + (X ? 1 : 0) + (P ? 4 : 0):                                                  \
+  case E * 16 + (NKV == 48 ? 2 : (NKV == 3 ? 1 : 0)) * 4 + (X ? 1 : 0) + (P ? 2 : 0):                           \
     hipLaunchKernelGGL((k_pg<E, NKV, X, P>), dim3(P ? (grid + 1) / 2 : grid), dim3(P ? 512 : 256),            \
                        P ? 2 * PG_LDS : PG_LDS, stream(), a, bp, (int)M, (int)N, (int)lda, tiles_n, nt, stg, e); \
     break;
@@ -1296,6 +1308,9 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     PGL(PG_GELU, 12, true, true)
     PGL(PG_RESID, 12, true, true) PGL(PG_RESID, 12, false, true) PGL(PG_RESID, 48, true, true)
     PGL(PG_RESID, 48, false, true)
+    PGL(PG_QKV, 3, true, false)  // K = 192 (ViT-Ti)
+    PGL(PG_GELU, 3, true, false)
+    PGL(PG_RESID, 3, true, false) PGL(PG_RESID, 3, false, false)
 #undef PGL
     default:
       return 0;

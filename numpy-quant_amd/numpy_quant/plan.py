@@ -744,14 +744,14 @@ def _pack_b(bt, bit_width=8):
 
 
 def _pack_pg(bt, bit_width=8, layout=0):
-    """The nqk_pack_pg image of a constant Bt [N][K] (int8 weights, K in {768, 3072},
-    N % 256 == 0; layout 0 for the int8-output epilogues QKV / GELU, 1 for the residual
-    epilogues), or None (NQK_NO_PG set, or a shape the persistent 16x16x64 GEMM does not
-    take)."""
+    """The nqk_pack_pg image of a constant Bt [N][K] (int8 weights, K in {192, 768, 3072},
+    N % 64 == 0, padded with zero columns to a multiple of 256; layout 0 for the int8-output
+    epilogues QKV / GELU, 1 for the residual epilogues), or None (NQK_NO_PG set, or a shape
+    the persistent 16x16x64 GEMM does not take)."""
     N, K = bt.shape
-    if bit_width != 8 or K not in (768, 3072) or N % 256 or os.environ.get("NQK_NO_PG"):
+    if bit_width != 8 or K not in (192, 768, 3072) or N % 64 or os.environ.get("NQK_NO_PG"):
         return None
-    out = DeviceArray((N, K), np.int8)
+    out = DeviceArray(((N + 255) // 256 * 256, K), np.int8)
     _lib.call("nqk_pack_pg", bt.vp, out.vp, N, K, K, layout)
     return out
 
