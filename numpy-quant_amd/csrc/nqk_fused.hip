@@ -2048,10 +2048,18 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
     const double rs = 1.0 / (double)scale;
     const int64_t lanes = rows * p.nleaf * 2;
     const unsigned grid = (unsigned)((lanes + 255) / 256);
-    if (p.nleaf == 8 && !getenv("NQK_LN_REG")) {  // rows through LDS: linear 1 KiB loads / stores per wave
-      const unsigned g8 = (unsigned)((rows + 15) / 16);
-      hipLaunchKernelGGL((k_ln_quant_lds<8>), dim3(g8), dim3(256), ln_lds_bytes(8), stream(), x, gamma, beta, out,
-                         rows, eps, scale, rs, (double)zp, lo, hi);
+    if (!getenv("NQK_LN_REG")) {  // rows through LDS: linear 1 KiB loads / stores per wave
+      // 128 / nleaf rows per workgroup (4 waves of 64 / (2 nleaf) rows)
+      const int64_t rpw = 128 / p.nleaf;
+      const unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
+      switch (p.nleaf) {
+        case 8: hipLaunchKernelGGL((k_ln_quant_lds<8>), dim3(gl), dim3(256), ln_lds_bytes(8), stream(), x, gamma, beta,
+                                   out, rows, eps, scale, rs, (double)zp, lo, hi); break;
+        case 4: hipLaunchKernelGGL((k_ln_quant_lds<4>), dim3(gl), dim3(256), ln_lds_bytes(4), stream(), x, gamma, beta,
+                                   out, rows, eps, scale, rs, (double)zp, lo, hi); break;
+        default: hipLaunchKernelGGL((k_ln_quant_lds<2>), dim3(gl), dim3(256), ln_lds_bytes(2), stream(), x, gamma,
+                                    beta, out, rows, eps, scale, rs, (double)zp, lo, hi); break;
+      }
       return launch_status("nqk_ln_quant(lds)");
     }
     switch (p.nleaf) {

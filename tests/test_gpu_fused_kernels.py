@@ -22,8 +22,13 @@ def _ln_ref(x, g, b, eps):
 @pytest.mark.parametrize("rows,cols", [(1, 768), (257, 768), (1000, 192), (33, 384), (64, 197), (5, 1000),
                                        (3, 96), (7, 3072)])
 @pytest.mark.parametrize("bw,zp", [(8, -3), (8, 140), (4, 2)])
-def test_ln_quant(rows, cols, bw, zp):
+@pytest.mark.parametrize("path", ["lds", "reg"])
+def test_ln_quant(rows, cols, bw, zp, path, monkeypatch):
     from numpy_quant import _lib
+    if path == "reg":
+        monkeypatch.setenv("NQK_LN_REG", "1")
+    else:
+        monkeypatch.delenv("NQK_LN_REG", raising=False)
     from numpy_quant.device import DeviceArray
     rng = np.random.default_rng(rows * cols + bw)
     x = (rng.standard_normal((rows, cols)) * 2 + 0.3).astype(np.float32)

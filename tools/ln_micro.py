@@ -15,7 +15,7 @@ from numpy_quant.device import DeviceArray  # noqa: E402
 if os.environ.get("GM_LIB"):
     _lib.LIB_PATH = os.environ["GM_LIB"]
 _lib.ensure_init()
-rows, cols = 256 * 197, 768
+rows, cols = 256 * 197, int(os.environ.get("LN_COLS", 768))
 rng = np.random.default_rng(0)
 x = DeviceArray.from_host(rng.standard_normal((rows, cols), dtype=np.float32))
 g = DeviceArray.from_host(np.ones(cols, np.float32))
