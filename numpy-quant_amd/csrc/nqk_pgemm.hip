@@ -72,6 +72,9 @@ enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fus
 #define NQK_PG_RLAUX -1  // cache-policy bits of the RESID epilogue's residual loads: -1 = nt for K = 3072
                          // (FFN-down 144 -> 138 us) and plain for K = 768 (nt: out-proj 59 -> 70 us)
 #endif
+#ifndef NQK_PG_GELU4
+#define NQK_PG_GELU4 1  // GELU epilogue two element pairs at a time, the chains interleaved
+#endif
 #ifndef NQK_PG_BREG
 #define NQK_PG_BREG 0  // 1: B fragments straight from L2 into VGPRs (buffer_load_dwordx4, one step ahead;
                        // parity-tested, measured no faster: profiles/r03h_pg_breg_dropped.txt)
@@ -276,6 +279,36 @@ __device__ __forceinline__ v2f gelu_fast2(v2f h) {
   const v2f ex = v2f{__builtin_amdgcn_exp2f(ea[0]), __builtin_amdgcn_exp2f(ea[1])};
   const v2f q = (p * t) * ex;
   return __builtin_elementwise_fma(-ah, q, __builtin_elementwise_max(h, v2f{0.0f, 0.0f}));
+}
+
+// gelu_fast2 on two element pairs with every step of the two chains side by side: the
+// dependent packed instructions of one chain leave hazard wait states (s_nop) that the other
+// chain's instruction fills (same operations per lane, same bits)
+__device__ __forceinline__ void gelu_fast2x2(v2f h0, v2f h1, v2f& g0, v2f& g1) {
+  const v2f c1 = v2f{0.3275911f * 0.70710677f, 0.3275911f * 0.70710677f}, one = v2f{1.0f, 1.0f};
+  const v2f ah0 = __builtin_elementwise_abs(h0), ah1 = __builtin_elementwise_abs(h1);
+  const v2f d0 = __builtin_elementwise_fma(c1, ah0, one), d1 = __builtin_elementwise_fma(c1, ah1, one);
+  const v2f hc0 = h0 * v2f{-0.72134752f, -0.72134752f}, hc1 = h1 * v2f{-0.72134752f, -0.72134752f};
+  const v2f t0 = v2f{__builtin_amdgcn_rcpf(d0[0]), __builtin_amdgcn_rcpf(d0[1])};
+  const v2f t1 = v2f{__builtin_amdgcn_rcpf(d1[0]), __builtin_amdgcn_rcpf(d1[1])};
+  const v2f ea0 = h0 * hc0, ea1 = h1 * hc1;
+  const v2f k5 = v2f{0.5f * 1.061405429f, 0.5f * 1.061405429f}, k4 = v2f{0.5f * -1.453152027f, 0.5f * -1.453152027f};
+  const v2f k3 = v2f{0.5f * 1.421413741f, 0.5f * 1.421413741f}, k2 = v2f{0.5f * -0.284496736f, 0.5f * -0.284496736f};
+  const v2f k1 = v2f{0.5f * 0.254829592f, 0.5f * 0.254829592f};
+  v2f p0 = __builtin_elementwise_fma(k5, t0, k4), p1 = __builtin_elementwise_fma(k5, t1, k4);
+  const v2f ex0 = v2f{__builtin_amdgcn_exp2f(ea0[0]), __builtin_amdgcn_exp2f(ea0[1])};
+  const v2f ex1 = v2f{__builtin_amdgcn_exp2f(ea1[0]), __builtin_amdgcn_exp2f(ea1[1])};
+  p0 = __builtin_elementwise_fma(p0, t0, k3);
+  p1 = __builtin_elementwise_fma(p1, t1, k3);
+  p0 = __builtin_elementwise_fma(p0, t0, k2);
+  p1 = __builtin_elementwise_fma(p1, t1, k2);
+  p0 = __builtin_elementwise_fma(p0, t0, k1);
+  p1 = __builtin_elementwise_fma(p1, t1, k1);
+  const v2f pt0 = p0 * t0, pt1 = p1 * t1;
+  const v2f q0 = pt0 * ex0, q1 = pt1 * ex1;
+  const v2f z = v2f{0.0f, 0.0f};
+  g0 = __builtin_elementwise_fma(-ah0, q0, __builtin_elementwise_max(h0, z));
+  g1 = __builtin_elementwise_fma(-ah1, q1, __builtin_elementwise_max(h1, z));
 }
 
 // Q_LIM = (0.5 - 2^-126)(1 - 2^-23) rounded down: a rounded fma measure below it keeps the
@@ -493,9 +526,37 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         uint32_t worst = 0;
         float hv[16];
         v2f sprev;
+        // GELU, two pairs at a time (NQK_PG_GELU4): the two chains interleaved
+        if constexpr (EPI == PG_GELU && NQK_PG_GELU4 && (NQK_PG_DIAG & 2) == 0) {
+#pragma unroll
+          for (int q = 0; q < 16; q += 4) {
+            const v4i& av4 = acc[i][q >> 2];
+            const v2f vf0 = v2f{(float)av4[0], (float)av4[1]}, vf1 = v2f{(float)av4[2], (float)av4[3]};
+            const v2f h0 = v2f{bias[q], bias[q + 1]} + vf0 * v2f{sacc, sacc};
+            const v2f h1 = v2f{bias[q + 2], bias[q + 3]} + vf1 * v2f{sacc, sacc};
+            hv[q] = h0[0];
+            hv[q + 1] = h0[1];
+            hv[q + 2] = h1[0];
+            hv[q + 3] = h1[1];
+            v2f g0, g1;
+            gelu_fast2x2(h0, h1, g0, g1);
+            const v2f tf0 = g0 * v2f{rsf, rsf}, tf1 = g1 * v2f{rsf, rsf};
+            v2f dd0, dd1;
+            const v2f s0 = round_magic2(tf0, qlo, qhi, magic, dd0);
+            const v2f s1 = round_magic2(tf1, qlo, qhi, magic, dd1);
+            const float m0 = __builtin_fmaf(__builtin_fabsf(h0[0]), e.g_rel, __builtin_fabsf(dd0[0]));
+            const float m1 = __builtin_fmaf(__builtin_fabsf(h0[1]), e.g_rel, __builtin_fabsf(dd0[1]));
+            const float m2 = __builtin_fmaf(__builtin_fabsf(h1[0]), e.g_rel, __builtin_fabsf(dd1[0]));
+            const float m3 = __builtin_fmaf(__builtin_fabsf(h1[1]), e.g_rel, __builtin_fabsf(dd1[1]));
+            worst = __builtin_elementwise_max(
+                worst, __builtin_elementwise_max(__builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)),
+                                                 __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3))));
+            pk[q >> 2] = pack4_low(s0, s1);
+          }
+        }
         // the fast paths on element pairs (packed f32 arithmetic where an instruction exists)
 #pragma unroll
-        for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) == 0; q += 2) {
+        for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) == 0 && !(EPI == PG_GELU && NQK_PG_GELU4); q += 2) {
           const v2f vf = v2f{(float)acc[i][q >> 2][q & 3], (float)acc[i][q >> 2][(q & 3) + 1]};
           v2f dd, sv;
           float m0, m1;
