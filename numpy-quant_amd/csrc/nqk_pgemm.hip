@@ -250,15 +250,19 @@ __device__ __forceinline__ void pg_exact_fix1(int q, const int (&av)[16], const 
 // a loop that is not unrolled (av / xv / pk indexed by the wave-uniform q stay in VGPRs via
 // relative moves), so the long exact chain is not duplicated per element and per step; QKV:
 // unrolled (its exact chain is short; measured faster, profiles/r03_pg_micro.txt).
+// gm (GELU with NQK_PG_GELU4): bit g set when some lane's filter measure of elements
+// 4 g .. 4 g + 3 failed; the other groups are skipped (their elements all passed)
 template <int EPI>
 __device__ __forceinline__ void pg_exact_fix(const int (&av)[16], const float (&xv)[16], uint32_t (&pk)[4],
-                                             const PgFix& f, const PgEpi& e) {
+                                             const PgFix& f, const PgEpi& e, uint32_t gm = 15u) {
   if constexpr (EPI == PG_QKV) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) pg_exact_fix1<EPI>(q, av, xv, pk, f, e);
   } else {
 #pragma clang loop unroll(disable)
-    for (int q = 0; q < 16; ++q) pg_exact_fix1<EPI>(q, av, xv, pk, f, e);
+    for (int q = 0; q < 16; ++q) {
+      if ((gm >> (q >> 2)) & 1u) pg_exact_fix1<EPI>(q, av, xv, pk, f, e);
+    }
   }
 }
 
@@ -524,6 +528,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         }
         uint32_t pk[4] = {0, 0, 0, 0};
         uint32_t worst = 0;
+        uint32_t wgr[4] = {0, 0, 0, 0};  // GELU4: the measure's maximum per group of 4 elements
         float hv[16];
         v2f sprev;
         // GELU, two pairs at a time (NQK_PG_GELU4): the two chains interleaved
@@ -548,9 +553,9 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
             const float m1 = __builtin_fmaf(__builtin_fabsf(h0[1]), e.g_rel, __builtin_fabsf(dd0[1]));
             const float m2 = __builtin_fmaf(__builtin_fabsf(h1[0]), e.g_rel, __builtin_fabsf(dd1[0]));
             const float m3 = __builtin_fmaf(__builtin_fabsf(h1[1]), e.g_rel, __builtin_fabsf(dd1[1]));
-            worst = __builtin_elementwise_max(
-                worst, __builtin_elementwise_max(__builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)),
-                                                 __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3))));
+            wgr[q >> 2] = __builtin_elementwise_max(__builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)),
+                                                    __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3)));
+            worst = __builtin_elementwise_max(worst, wgr[q >> 2]);
             pk[q >> 2] = pack4_low(s0, s1);
           }
         }
@@ -604,7 +609,13 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
               av[q] = acc[i][q >> 2][q & 3];
               xv[q] = EPI == PG_QKV ? bias[q] : hv[q];
             }
-            pg_exact_fix<EPI>(av, xv, pk, PgFix{c1, k1, rsf, sacc, lim, s_out, rs_out, zp}, e);
+            uint32_t gm = 15u;
+            if constexpr (EPI == PG_GELU && NQK_PG_GELU4) {
+              gm = 0u;
+#pragma unroll
+              for (int g = 0; g < 4; ++g) gm |= __any(wgr[g] >= __float_as_uint(lim)) ? 1u << g : 0u;
+            }
+            pg_exact_fix<EPI>(av, xv, pk, PgFix{c1, k1, rsf, sacc, lim, s_out, rs_out, zp}, e, gm);
           }
         }
         const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};

@@ -1,0 +1,11 @@
+# GELU exact fallback restricted to the element groups whose filter measure failed (main)
+# vs the previous k_pg (hold) and a build without any exact fallback (e32: wrong results,
+# timing only): GEMM / model parity on main, then a same-box bench A/B
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_pgemm.py tests/test_gpu_kernels.py tests/test_gpu_b256.py tests/test_gpu_plan.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r3_gskip_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/r3_gskip_tests.log
+tail -3 gpurun_out/r3_gskip_tests.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+AB_LIBS="hold e32" bash tools/r3_bench_ab.sh
