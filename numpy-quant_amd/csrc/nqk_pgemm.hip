@@ -250,14 +250,19 @@ __device__ __forceinline__ void pg_exact_fix1(int q, const int (&av)[16], const 
 // a loop that is not unrolled (av / xv / pk indexed by the wave-uniform q stay in VGPRs via
 // relative moves), so the long exact chain is not duplicated per element and per step; QKV:
 // unrolled (its exact chain is short; measured faster, profiles/r03_pg_micro.txt).
-// gm (GELU with NQK_PG_GELU4): bit g set when some lane's filter measure of elements
+// gm (QKV, and GELU with NQK_PG_GELU4): bit g set when some lane's filter measure of elements
 // 4 g .. 4 g + 3 failed; the other groups are skipped (their elements all passed)
 template <int EPI>
 __device__ __forceinline__ void pg_exact_fix(const int (&av)[16], const float (&xv)[16], uint32_t (&pk)[4],
                                              const PgFix& f, const PgEpi& e, uint32_t gm = 15u) {
   if constexpr (EPI == PG_QKV) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) pg_exact_fix1<EPI>(q, av, xv, pk, f, e);
+    for (int g = 0; g < 4; ++g) {
+      if ((gm >> g) & 1u) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pg_exact_fix1<EPI>(4 * g + j, av, xv, pk, f, e);
+      }
+    }
   } else {
 #pragma clang loop unroll(disable)
     for (int q = 0; q < 16; ++q) {
@@ -528,7 +533,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         }
         uint32_t pk[4] = {0, 0, 0, 0};
         uint32_t worst = 0;
-        uint32_t wgr[4] = {0, 0, 0, 0};  // GELU4: the measure's maximum per group of 4 elements
+        uint32_t wgr[4] = {0, 0, 0, 0};  // QKV, GELU4: the measure's maximum per group of 4 elements
         float hv[16];
         v2f sprev;
         // GELU, two pairs at a time (NQK_PG_GELU4): the two chains interleaved
@@ -584,7 +589,10 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
             m0 = __builtin_fmaf(__builtin_fabsf(h[0]), e.g_rel, __builtin_fabsf(dd[0]));
             m1 = __builtin_fmaf(__builtin_fabsf(h[1]), e.g_rel, __builtin_fabsf(dd[1]));
           }
-          worst = __builtin_elementwise_max(worst, __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
+          if constexpr (EPI == PG_QKV)
+            wgr[q >> 2] = __builtin_elementwise_max(wgr[q >> 2], __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
+          else
+            worst = __builtin_elementwise_max(worst, __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
           if constexpr (EPI != PG_QKV) {
             if (q & 2) pk[q >> 2] = pack4_low(sprev, sv);
             sprev = sv;
@@ -593,6 +601,8 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         if constexpr (EPI == PG_QKV) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) pk[g] ^= 0x80808080u;  // offset bytes to two's complement
+          worst = __builtin_elementwise_max(__builtin_elementwise_max(wgr[0], wgr[1]),
+                                            __builtin_elementwise_max(wgr[2], wgr[3]));
         }
 #pragma unroll
         for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) != 0; ++q)  // diagnostic: no epilogue math
@@ -610,7 +620,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
               xv[q] = EPI == PG_QKV ? bias[q] : hv[q];
             }
             uint32_t gm = 15u;
-            if constexpr (EPI == PG_GELU && NQK_PG_GELU4) {
+            if constexpr (EPI == PG_QKV || (EPI == PG_GELU && NQK_PG_GELU4)) {
               gm = 0u;
 #pragma unroll
               for (int g = 0; g < 4; ++g) gm |= __any(wgr[g] >= __float_as_uint(lim)) ? 1u << g : 0u;
