@@ -246,6 +246,10 @@ typedef struct nqk_epilogue {
   const int8_t* bt_pg;                  /* optional: the nqk_pack_pg image of the same Bt;  */
                                         /* when set, the 16x16x64 persistent GEMM (k_pg)  */
                                         /* runs the cases it takes (NULL: not used)       */
+  const void* gelu_lut;                 /* optional (EPI_GELU with bt_pg): the table of    */
+  float lut_k[5];                       /* nqk_gelu_lut_build, its bucket coordinate and   */
+  int32_t lut_n;                        /* entry count; k_pg then looks the GELU chain's   */
+                                        /* output bytes up instead of computing them       */
 } nqk_epilogue;
 /* int8 MFMA GEMM C = A . Bt^T (layouts as nqk_qgemm_i8) with a fused epilogue:
  *   QKV    model.py MatMul -> Add(bias) -> Reshape -> Transpose -> quantize, 3 groups
@@ -271,6 +275,25 @@ int nqk_pack_b4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t ld
  * residual epilogues, f32 outputs); ceil(N/256)*256*K bytes (a layout of the
  * numpy_quantization.py:44-61 q_matmul operand, replaces no reference function). */
 int nqk_pack_pg(const int8_t* bt, int8_t* out, int64_t N, int64_t K, int64_t ldb, int layout);
+/* int4 weights (every value in [-8, 7], bit width <= 4): the same stages nibble-packed, 256 rows
+ * x 32 bytes each, ceil(N/256)*256*K/2 bytes; k_pg unpacks them in registers after the LDS stage
+ * (nqk_epilogue.b_packed = 2 with bt_pg = this image).  BASELINE configs[4]. */
+int nqk_pack_pg4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t ldb, int layout);
+/* The FFN-up epilogue's GELU chain as a table (round 4): model.py Div -> Erf -> Add -> Mul ->
+ * Mul on f32 (numpy_helper.py:95-112 erf) followed by numpy_quantization.py:24-34 quantize
+ * with (s_out, zp_out, bit_width), as a step function of the dequantized, biased f32 value h:
+ * at most 512 buckets of 8 bytes in lut (a 4 KiB, 16-byte aligned device buffer), the bucket
+ * coordinate in k_out[5], the entry count in *n_out.  Every entry comes from the exact chain,
+ * and the table is then compared with the exact chain on all 2^32 - 2^24 finite f32 inputs:
+ * *n_out = 0 (return 0) when the table cannot represent the chain exactly, when the chain is
+ * not the GELU of model.py (div = f32(sqrt 2), add1 = 1, mul2 = 0.5) or bit_width is not in
+ * 2..8.  Blocking (plan build time). */
+int nqk_gelu_lut_build(float s_out, int64_t zp_out, int32_t bit_width, float div, float add1, float mul2, void* lut,
+                       float* k_out, int32_t* n_out);
+/* The number of finite f32 inputs on which a table (n entries, coordinate k) differs from the
+ * exact chain (tests). */
+int nqk_gelu_lut_check(float s_out, int64_t zp_out, int32_t bit_width, float div, float add1, float mul2,
+                       const void* lut, const float* k, int32_t n, uint64_t* mismatches);
 int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, int64_t M, int64_t N, int64_t K,
                     int64_t lda, int64_t ldb, const int64_t* bmap, int64_t a_mat_stride, int64_t b_mat_stride,
                     const nqk_epilogue* params);
@@ -278,7 +301,8 @@ int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, i
  * (k_qgemm_epi), 1 128x256 tiles (k_qgemm_big), 2 ping-pong 256x256 (k_qgemm_pp), 3 the
  * persistent projection GEMM with the epilogue overlapped (k_proj), 4 the persistent 16x16x64
  * GEMM with two workgroups per CU (k_pg), 5 the persistent 16x16x64 GEMM with each tile's
- * epilogue inside the next tile's k loop (k_pg2); -1 none yet. */
+ * epilogue inside the next tile's k loop (k_pg2), 6 k_pg with the GELU table epilogue
+ * (nqk_gelu_lut_build); -1 none yet. */
 int nqk_qgemm_last_kernel(void);
 /* LayerNormalization (model.py:134-152) fused with the consumer MatMul's quantize */
 int nqk_ln_quant(const float* x, const float* gamma, const float* beta, int8_t* out, int64_t rows, int64_t cols,

@@ -1,0 +1,277 @@
+// Builder and exhaustive check of the GELU lookup table of the FFN-up GEMM epilogue
+// (nqk_glut.h; the k_pg GELU epilogue in nqk_pgemm.hip reads it from LDS).
+// Reference chain: model.py Div / Erf / Add / Mul / Mul on f32 (numpy_helper.py:95-112),
+// then numpy_quantization.py:24-34 quantize.
+#include <cmath>
+#include <vector>
+
+#include "nqk_common.h"
+#include "nqk_glut.h"
+
+namespace nqk {
+namespace {
+
+struct GLutQ {  // the quantize of the GELU output and the chain's constants
+  double rdiv, rs, zp, lo, hi;
+  float add1, mul2;
+};
+
+__device__ __forceinline__ int glut_q(float h, const GLutQ& q) {
+  return glut_exact(h, q.rdiv, q.add1, q.mul2, q.rs, q.zp, q.lo, q.hi) & 0xff;
+}
+__device__ __forceinline__ int glut_idx(float h, const GLutK& k) {
+  return (int)(__float_as_uint(glut_u(h, k)) - GLUT_MAGIC_BITS);
+}
+// floats in increasing order <-> uint32 keys (-0 just below +0)
+__device__ __forceinline__ uint32_t okey(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ofloat(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+// smallest key in [a, b] where pred turns true (pred monotone false -> true); b + 1 if never
+template <typename P>
+__device__ uint64_t first_true(uint32_t a, uint32_t b, P&& pred) {
+  uint64_t lo = a, hi = (uint64_t)b + 1;  // pred(hi) taken as true
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (pred(ofloat((uint32_t)mid))) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+// one thread per bucket: the bucket's h range [lo, hi] (keys), its output byte at both ends,
+// the first h where the byte changes (bisection, assuming at most one change: the check below
+// rejects the table otherwise) and the window of floats after it where the f32 chain still
+// alternates (the last of up to 256 floats whose output differs from the bucket's end)
+__global__ void k_glut_build(uint2* __restrict__ lut, int n, GLutK k, GLutQ q, unsigned* __restrict__ err) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  const uint32_t kmin = okey(-3.40282347e38f), kmax = okey(3.40282347e38f);
+  const uint64_t lo = b == 0 ? kmin : first_true(kmin, kmax, [&](float h) { return glut_idx(h, k) >= b; });
+  const uint64_t nx = b == n - 1 ? (uint64_t)kmax + 1 : first_true(kmin, kmax, [&](float h) { return glut_idx(h, k) >= b + 1; });
+  uint2 ent = make_uint2(0x7f800000u, 0u);  // empty bucket (never indexed); no change: thr = +inf, K = 0
+  if (lo < nx) {
+    const uint32_t klo = (uint32_t)lo, khi = (uint32_t)(nx - 1);
+    const int q0 = glut_q(ofloat(klo), q), q1 = glut_q(ofloat(khi), q);
+    ent.y = (uint32_t)q0 | ((uint32_t)q1 << 16);
+    if (q0 != q1) {
+      const uint32_t ka = (uint32_t)first_true(klo, khi, [&](float h) { return glut_q(h, q) != q0; });
+      uint32_t kb = ka;
+      for (uint32_t j = 1; j < 256 && ka + j <= khi; ++j)
+        if (glut_q(ofloat(ka + j), q) != q1) kb = ka + j;
+      const float fa = ofloat(ka), fb = ofloat(kb);
+      const uint32_t ba = __float_as_uint(fa), bb = __float_as_uint(fb);
+      if (!(ba >> 31) && !(bb >> 31)) {  // a, b >= +0: anchored at a
+        ent.x = ba;
+        ent.y |= (bb - ba) << 8;
+      } else if ((ba >> 31) && (bb >> 31)) {  // a, b <= -0: anchored at b
+        ent.x = bb;
+        ent.y |= (ba - bb) << 8;
+      } else {
+        atomicAdd(err, 1u);  // a window across zero: not representable
+      }
+    }
+  }
+  lut[b] = ent;
+}
+
+// every finite f32 h outside the windows: table lookup == exact chain; per bucket the number
+// of mismatches and their smallest / largest key (the host widens windows from these)
+struct GLutBad {
+  unsigned long long total;
+  unsigned cnt[GLUT_MAX], kmin[GLUT_MAX], kmax[GLUT_MAX];
+};
+__global__ void __launch_bounds__(256) k_glut_verify(const uint2* __restrict__ lut, int n, GLutK k, GLutQ q,
+                                                     GLutBad* __restrict__ bad) {
+  __shared__ uint2 tab[GLUT_MAX];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) tab[i] = lut[i];
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned long long nbad = 0;
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < (1ull << 32); x += stride) {
+    const uint32_t bits = (uint32_t)x;
+    if ((bits & 0x7f800000u) == 0x7f800000u) continue;  // inf / NaN: h is always finite
+    const float h = __uint_as_float(bits);
+    const int i = glut_idx(h, k);
+    const uint2 e = tab[i];
+    if (glut_in_window(h, e.x, e.y)) continue;  // the epilogue's exact path
+    if (glut_pick(h, e.x, e.y) != (uint32_t)glut_q(h, q)) {
+      ++nbad;
+      atomicAdd(&bad->cnt[i], 1u);
+      atomicMin(&bad->kmin[i], okey(h));
+      atomicMax(&bad->kmax[i], okey(h));
+    }
+  }
+  if (nbad) atomicAdd(&bad->total, nbad);
+}
+
+double gelu_d(double h) { return 0.5 * h * (1.0 + std::erf(h / std::sqrt(2.0))); }
+// h on [a, b] where the monotone gelu_d crosses y (bisection; a < b)
+double gelu_solve(double a, double b, double y) {
+  const bool inc = gelu_d(b) > gelu_d(a);
+  for (int i = 0; i < 200; ++i) {
+    const double m = 0.5 * (a + b);
+    if ((gelu_d(m) < y) == inc) a = m;
+    else b = m;
+  }
+  return 0.5 * (a + b);
+}
+
+}  // namespace
+
+// Build the table for one GELU epilogue (nqk.h).  The bucket grid comes from double-precision
+// GELU (sizing only); every entry comes from the exact f32 chain on the device, and the whole
+// table is then compared with that chain on all finite f32 inputs.
+extern "C" int nqk_gelu_lut_build(float s_out, int64_t zp_out, int32_t bit_width, float div, float add1, float mul2,
+                                  void* lut, float* k_out, int32_t* n_out) {
+  if (!n_out || !k_out) return fail("nqk_gelu_lut_build: null output");
+  *n_out = 0;
+  if (!lut || (((uintptr_t)lut) & 15)) return fail("nqk_gelu_lut_build: lut must be a 16-byte aligned device buffer");
+  if (bit_width < 2 || bit_width > 8) return 0;  // output bytes: bit widths 2..8 only
+  if (!(std::fabs(s_out) >= 0x1p-100f && std::fabs(s_out) <= 0x1p100f) || s_out < 0.0f) return 0;
+  if (zp_out < -(1 << 20) || zp_out > (1 << 20)) return 0;
+  if (!(div == 1.41421354f && add1 == 1.0f && mul2 == 0.5f)) return 0;  // the GELU structure of model.py
+  const double s = s_out, zp = (double)zp_out;
+  const double lo = -std::ldexp(1.0, bit_width - 1), hi = std::ldexp(1.0, bit_width - 1) - 1.0;
+  const double hk = -0.7517915246170625;  // argmin of GELU
+  const double gmin = gelu_d(hk);
+  // right end: where the output saturates at hi; left end: where it leaves zp on the decreasing branch
+  const double yr = (hi + 0.5 - zp) * s, yl = -0.5 * s;
+  double hr = yr <= gmin ? hk + 1e-3 : (yr >= gelu_d(1e6) ? 1e6 : gelu_solve(hk, 1e6, yr));
+  double hl = yl <= gmin ? hk - 1e-3 : gelu_solve(-40.0, hk, yl);
+  // bucket widths below the closest spacing of two output steps on each branch (max slope
+  // 1.129 on the increasing branch, 0.129 on the decreasing one)
+  double wl = 3.0 * s;
+  int n = 0, nl = 0;
+  double wr = 0.0;
+  for (double f : {0.75, 0.85}) {
+    wr = f * s;
+    nl = (int)std::ceil((hk - (hl - 2.0 * wl)) / wl);
+    const int nr = (int)std::ceil(((hr + 2.0 * wr) - hk) / wr);
+    n = nl + nr + 2;
+    if (n <= GLUT_MAX) break;
+  }
+  if (n > GLUT_MAX || n < 3) return 0;
+  const double M = GLUT_MAGIC;
+  GLutK k;
+  k.iwR = (float)(1.0 / wr);
+  k.cR = (float)(M + nl + 1 - hk * (double)k.iwR);
+  k.iwL = (float)(1.0 / wl);
+  k.cL = (float)(M + nl + 1 - hk * (double)k.iwL);
+  k.uhi = (float)(M + n - 1);
+  GLutQ q;
+  q.rdiv = 1.0 / (double)div;
+  q.rs = 1.0 / (double)s_out;
+  q.zp = zp;
+  q.lo = lo;
+  q.hi = hi;
+  q.add1 = add1;
+  q.mul2 = mul2;
+  // device scratch: the build's error count and the check's per-bucket mismatch record
+  GLutBad* bad = nullptr;
+  unsigned* err = nullptr;
+  if (int rc = check(hipMalloc((void**)&bad, sizeof(GLutBad) + 16), "nqk_gelu_lut_build(alloc)")) return rc;
+  err = reinterpret_cast<unsigned*>(bad + 1);
+  auto done = [&](int rc) {
+    (void)hipFree(bad);
+    return rc;
+  };
+  int rc = check(hipMemsetAsync(err, 0, 4, stream()), "nqk_gelu_lut_build(memset)");
+  if (rc) return done(rc);
+  hipLaunchKernelGGL(k_glut_build, dim3((n + 63) / 64), dim3(64), 0, stream(), (uint2*)lut, n, k, q, err);
+  if ((rc = launch_status("nqk_gelu_lut_build(build)"))) return done(rc);
+  unsigned herr = 0;
+  if ((rc = check(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream()), "nqk_gelu_lut_build(copy)"))) return done(rc);
+  // check; where a bucket's mismatches lie within 256 floats next to its window (or, in a
+  // bucket without a change, anywhere), widen / place the window over them and check again
+  std::vector<uint2> tab(n);
+  auto verify = [&](GLutBad& hb) {
+    int r = check(hipMemsetAsync(bad, 0, sizeof(GLutBad), stream()), "nqk_gelu_lut_build(memset)");
+    if (!r) r = check(hipMemsetAsync(bad->kmin, 0xff, sizeof(unsigned) * GLUT_MAX, stream()), "nqk_gelu_lut_build(memset)");
+    if (r) return r;
+    hipLaunchKernelGGL(k_glut_verify, dim3(2048), dim3(256), 0, stream(), (const uint2*)lut, n, k, q, bad);
+    if ((r = launch_status("nqk_gelu_lut_build(verify)"))) return r;
+    if ((r = check(hipMemcpyAsync(&hb, bad, sizeof(GLutBad), hipMemcpyDeviceToHost, stream()), "nqk_gelu_lut_build(copy)")))
+      return r;
+    return check(hipStreamSynchronize(stream()), "nqk_gelu_lut_build(sync)");
+  };
+  GLutBad hb;
+  for (int pass = 0; pass < 2 && !herr; ++pass) {
+    if ((rc = verify(hb))) return done(rc);
+    if (hb.total == 0) {
+      k_out[0] = k.iwR;
+      k_out[1] = k.cR;
+      k_out[2] = k.iwL;
+      k_out[3] = k.cL;
+      k_out[4] = k.uhi;
+      *n_out = n;
+      return done(0);
+    }
+    if (pass == 1) break;
+    if ((rc = check(hipMemcpy(tab.data(), lut, 8 * (size_t)n, hipMemcpyDeviceToHost), "nqk_gelu_lut_build(read)")))
+      return done(rc);
+    bool ok = true;
+    for (int i = 0; i < n && ok; ++i) {
+      if (!hb.cnt[i]) continue;
+      auto fl = [](unsigned key) {  // key -> float bits
+        return (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+      };
+      auto key_of = [](uint32_t bits) { return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u); };
+      unsigned lo = hb.kmin[i], hi = hb.kmax[i];
+      const uint32_t thr = tab[i].x, K = (tab[i].y >> 8) & 0xffu;
+      const bool has_change = (tab[i].y & 0xffu) != ((tab[i].y >> 16) & 0xffu);
+      if (has_change) {  // the existing window in keys
+        const bool neg = thr >> 31;
+        const unsigned wa = neg ? key_of(thr + K) : key_of(thr), wb = neg ? key_of(thr) : key_of(thr + K);
+        lo = lo < wa ? lo : wa;
+        hi = hi > wb ? hi : wb;
+      }
+      const uint32_t fa = fl(lo), fb = fl(hi);
+      if (hi - lo > 255 || ((fa >> 31) != (fb >> 31))) {
+        ok = false;
+        break;
+      }
+      const bool neg = fa >> 31;
+      tab[i].x = neg ? fb : fa;
+      tab[i].y = (tab[i].y & 0xffff00ffu) | ((neg ? fa - fb : fb - fa) << 8);
+    }
+    if (!ok) break;
+    if ((rc = check(hipMemcpy(lut, tab.data(), 8 * (size_t)n, hipMemcpyHostToDevice), "nqk_gelu_lut_build(write)")))
+      return done(rc);
+  }
+  return done(0);  // *n_out = 0: the filtered chain stays
+}
+
+// diagnostics / tests: the mismatch count of a table (built by nqk_gelu_lut_build or altered)
+extern "C" int nqk_gelu_lut_check(float s_out, int64_t zp_out, int32_t bit_width, float div, float add1, float mul2,
+                                  const void* lut, const float* kin, int32_t n, uint64_t* mismatches) {
+  if (!lut || !kin || !mismatches || n < 1 || n > GLUT_MAX) return fail("nqk_gelu_lut_check: bad arguments");
+  GLutK k{kin[0], kin[1], kin[2], kin[3], kin[4]};
+  GLutQ q;
+  q.rdiv = 1.0 / (double)div;
+  q.rs = 1.0 / (double)s_out;
+  q.zp = (double)zp_out;
+  q.lo = -std::ldexp(1.0, bit_width - 1);
+  q.hi = std::ldexp(1.0, bit_width - 1) - 1.0;
+  q.add1 = add1;
+  q.mul2 = mul2;
+  GLutBad* bad = nullptr;
+  if (int rc = check(hipMalloc((void**)&bad, sizeof(GLutBad)), "nqk_gelu_lut_check(alloc)")) return rc;
+  GLutBad hb;
+  int rc = check(hipMemsetAsync(bad, 0, sizeof(GLutBad), stream()), "nqk_gelu_lut_check(memset)");
+  if (!rc) {
+    hipLaunchKernelGGL(k_glut_verify, dim3(2048), dim3(256), 0, stream(), (const uint2*)lut, n, k, q, bad);
+    rc = launch_status("nqk_gelu_lut_check");
+  }
+  if (!rc) rc = check(hipMemcpyAsync(&hb, bad, sizeof(GLutBad), hipMemcpyDeviceToHost, stream()), "nqk_gelu_lut_check(copy)");
+  if (!rc) rc = check(hipStreamSynchronize(stream()), "nqk_gelu_lut_check(sync)");
+  (void)hipFree(bad);
+  if (rc) return rc;
+  *mismatches = hb.total;
+  return 0;
+}
+
+}  // namespace nqk

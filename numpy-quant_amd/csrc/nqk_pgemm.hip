@@ -30,6 +30,7 @@
 
 #include "nqk_common.h"
 #include "nqk_numerics.h"
+#include "nqk_glut.h"
 
 namespace nqk {
 #if (NQK_PG_DIAG & 64)
@@ -46,6 +47,7 @@ namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -58,6 +60,16 @@ constexpr int PG_LDS = PG_COLP + 2 * 2048;       // 76 KiB: two workgroups per C
 constexpr int PG_PW = 2 + 4;                      // LDS-DMA pieces per wave per stage
 
 enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fused.hip
+constexpr int PG_GLUT = 5;  // GELU by table lookup (nqk_glut.h): launched for PG_GELU when a table is given
+// k_pg's LDS: a 3-stage ring of A (128 x 64 B) + B (256 rows x 64 B, or 32 B of int4
+// nibbles) per stage, the column constants (2 x 2 KiB), then the GELU table (PG_GLUT, 4 KiB)
+// or, for int4 weights, the residual epilogue's transpose scratch (int8: ring slot 2)
+constexpr int PG_TR_ROW = 272;  // bytes per staged residual row (256 + 16: conflict-free b128 writes)
+constexpr int pg_stg(bool b4) { return PG_ASTG + PG_BN * (b4 ? PG_BK / 2 : PG_BK); }
+constexpr int pg_colp(bool b4) { return PG_RD * pg_stg(b4); }
+constexpr int pg_lds_bytes(int epi, bool b4) {
+  return pg_colp(b4) + 4096 + (epi == PG_GLUT ? 8 * GLUT_MAX : 0) + (b4 && epi == PG_RESID ? 4 * 16 * PG_TR_ROW : 0);
+}
 
 #ifndef NQK_PG_STAUX
 #define NQK_PG_STAUX 2  // cache-policy bits of the epilogue's output stores: nt (profiles/r03c_*: out-proj
@@ -72,16 +84,11 @@ enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fus
 #define NQK_PG_RLAUX -1  // cache-policy bits of the RESID epilogue's residual loads: -1 = nt for K = 3072
                          // (FFN-down 144 -> 138 us) and plain for K = 768 (nt: out-proj 59 -> 70 us)
 #endif
+#ifndef NQK_PG_SPREAD
+#define NQK_PG_SPREAD 0  // 1: the stage's LDS-DMA pieces spread over the first half step (A/B variant)
+#endif
 #ifndef NQK_PG_GELU4
 #define NQK_PG_GELU4 1  // GELU epilogue two element pairs at a time, the chains interleaved
-#endif
-#ifndef NQK_PG_BREG
-#define NQK_PG_BREG 0  // 1: B fragments straight from L2 into VGPRs (buffer_load_dwordx4, one step ahead;
-                       // parity-tested, measured no faster: profiles/r03h_pg_breg_dropped.txt)
-                       // instead of LDS-DMA + ds_read (the wave's 64 weight columns are its own)
-#endif
-#ifndef NQK_PG_PAIR_DEFAULT
-#define NQK_PG_PAIR_DEFAULT 0  // k_pg as 512-thread two-half workgroups (NQK_PG_PAIR=0/1 at run time)
 #endif
 #ifndef NQK_PG_PRIO
 #define NQK_PG_PRIO 3  // 3: s_setprio 1 in the epilogue, 0 in the k loop (the epilogue's VALU ahead of the
@@ -144,6 +151,11 @@ __device__ __forceinline__ v4i pg_lds16o(const int8_t* base) {
     return *reinterpret_cast<const v4i*>(base + OFF);  // the offset folds into the instruction
   }
 }
+// ds_read_b64 at base + a compile-time byte offset (the int4 weight fragments)
+template <int OFF>
+__device__ __forceinline__ v2u pg_lds8o(const int8_t* base) {
+  return *reinterpret_cast<const v2u*>(base + OFF);
+}
 __device__ __forceinline__ void pg_lgkm() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -152,6 +164,11 @@ __device__ __forceinline__ void pg_lgkm() {
 // above the wait (a plain wait orders only memory operations)
 __device__ __forceinline__ void pg_lgkm_tie(v4i& a, v4i& b, v4i& c, v4i& d) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void pg_lgkm_tie_a4(v4i (&a)[4], v2u (&b)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
   __builtin_amdgcn_sched_barrier(0);
 }
 __device__ __forceinline__ void pg_lgkm_tie8(v4i (&a)[4], v4i (&b)[4]) {
@@ -197,6 +214,9 @@ struct PgEpi {
   float div, add1, mul2;
   double rdiv;
   int ldo;  // row stride (elements) of the GELU / RESID output
+  const void* lut;  // PG_GLUT: the GELU table (nqk_gelu_lut_build) and its bucket coordinate
+  GLutK gk;
+  float blo, bhi;   // QKV: the clamp of v + 128 ([lo + 128, hi + 128] of the bit width)
 };
 
 // quantize (numpy_quantization.py:24-34) with f64 zero-point add and clipping
@@ -325,62 +345,48 @@ __device__ __forceinline__ void gelu_fast2x2(v2f h0, v2f h1, v2f& g0, v2f& g1) {
 constexpr float PG_QLIM = 0x1.fffffcp-2f;
 
 
-// PAIR: one 512-thread workgroup per CU made of two independent 4-wave halves (each with
-// its own 76 KiB of LDS and its own tile sequence) that share the k-loop barriers, so the
-// two waves of every SIMD run their k loops and their epilogues at the same time.  Two
-// separate workgroups drift into alternating phases, and then a SIMD runs one wave's
-// epilogue VALU alone at the single-wave issue rate (one instruction per 4 cycles) beside
-// an MFMA stream that does not overlap it (profiles/r03d_*: MFMA + GELU epilogue without
-// loads = the sum of the two); two waves in their epilogues together issue every 2 cycles.
-template <int EPI, int NK, bool F32X, bool PAIR>
-__global__ void __launch_bounds__(PAIR ? 512 : 256, PAIR ? 1 : 2)
+// B4: int4 weights (every value in [-8, 7]) as the nibble image of nqk_pack_pg4: a stage's
+// B part is 256 rows x 32 bytes (half the LDS-DMA pieces and LDS bytes); a lane's 16 k-values
+// of one MFMA operand are 8 bytes (ds_read_b64) that unpack with two AND masks into bytes
+// 16 w (the nibble in the high half, its sign bit on the byte's; as nqk_fused.hip
+// k_qgemm_big), so the MFMAs accumulate 16 acc exactly (initial accumulators 16 x the column
+// terms, host-checked to fit int32) and the epilogue takes acc >> 4.
+template <int EPI, int NK, bool F32X, bool B4>
+__global__ void __launch_bounds__(256, 2)
 k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
-     int stagger, PgEpi e) {
+     PgEpi e) {
   static_assert(NK % PG_RD == 0 && (NK >= 2 * PG_RD || NK == PG_RD), "k_pg: NK a multiple of the ring depth");
   constexpr bool RESID = EPI == PG_RESID;
-  extern __shared__ __attribute__((aligned(16))) int8_t lds_all[];
+  constexpr int BROW = B4 ? PG_BK / 2 : PG_BK;  // bytes of one B row per k-step
+  constexpr int NBP = B4 ? 2 : 4;               // B LDS-DMA pieces per wave per stage
+  constexpr int STG = pg_stg(B4), COLP = pg_colp(B4), LUTO = COLP + 4096;
+  constexpr int PW = 2 + NBP;                   // LDS-DMA pieces per wave per stage
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
-  const int wg_half = PAIR ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
-  int8_t* const lds = lds_all + wg_half * PG_LDS;
   const int l15 = lane & 15, lg = lane >> 4;
 
   // tiles: the workgroups with blockIdx % 8 == x (one XCD under round-robin placement)
   // walk the band [lo, hi) of tile ids, every nx-th tile from lo + jx; tile ids are
   // row-panel major, so the tiles in flight on an XCD share A row panels in its L2.
-  // PAIR: the halves are virtual workgroups 2 j and 2 j + 1 of the same XCD.
   const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X;
-  const int nx = (PAIR ? 2 : 1) * ((G - x + X - 1) / X);
-  const int jx0 = (PAIR ? 2 : 1) * (blockIdx.x / X);
+  const int nx = (G - x + X - 1) / X;
   const int lo = (int)((int64_t)ntiles * x / X), hi = (int)((int64_t)ntiles * (x + 1) / X);
-  auto count_of = [&](int f) { return f < hi ? (hi - f + nx - 1) / nx : 0; };
-  int first = lo + jx0 + wg_half;
-  int cnt = count_of(first);
-  int iters = cnt;
-  if constexpr (PAIR) {
-    // both halves run the longer half's count (same barriers); a shorter half repeats its
-    // last tile, a half without tiles recomputes the other's (identical values rewritten)
-    iters = count_of(lo + jx0);
-    if (cnt == 0) {
-      first = lo + jx0;
-      cnt = iters;
-    }
-  }
+  const int first = lo + (int)(blockIdx.x / X);
+  const int iters = first < hi ? (hi - first + nx - 1) / nx : 0;
   if (iters == 0) return;
-  auto tile_at = [&](int it) { return first + (it < cnt ? it : cnt - 1) * nx; };
-  // the second workgroup of a CU (under round-robin placement: blockIdx >= G / 2) starts
-  // about half a tile later, so that the two workgroups' epilogues do not coincide
-  if (!PAIR && stagger > 0 && (int)blockIdx.x >= G / 2)
-    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(8);  // ~512 cycles each
+  auto tile_at = [&](int it) { return first + (it < iters ? it : iters - 1) * nx; };
 
-  constexpr int64_t BSTRIDE = (int64_t)NK * PG_BN * PG_BK;  // bytes of one column panel
+  constexpr int64_t BSTRIDE = (int64_t)NK * PG_BN * BROW;  // bytes of one column panel
   const rsrc_t r_a = pg_rsrc(A, (uint32_t)((uint64_t)M * lda));
   const rsrc_t r_b = pg_rsrc(Bp, (uint32_t)((uint64_t)tiles_n * BSTRIDE));
   // LDS-DMA sources: A piece pp of wave w = rows 32 w + 16 pp + (l >> 2), physical chunk l & 3
   const uint32_t va = (uint32_t)((32 * wave + (lane >> 2)) * lda + 16 * ((lane & 3) ^ pg_sw(lane >> 2)));
-  const uint32_t vb = (uint32_t)(4096 * wave + 16 * lane);
-  // fragment offsets: row (l & 15) of a 16-row subtile, logical chunk l >> 4
+  const uint32_t vb = (uint32_t)(NBP * 1024 * wave + 16 * lane);
+  // fragment offsets: row (l & 15) of a 16-row subtile, logical chunk l >> 4 (B4: 8-byte
+  // chunks of 32-byte rows, chunk ^ 2 in rows 8..15 of a subtile: conflict-free b64 reads)
   const int f_off = l15 * 64 + 16 * (lg ^ pg_sw(l15));
+  const int f_off4 = l15 * 32 + 8 * (lg ^ (2 * ((l15 >> 3) & 1)));
 
   struct Src { uint32_t sa, sb; int r0, tn; };
   auto src_of = [&](int tile) __attribute__((always_inline)) {
@@ -394,25 +400,29 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     s.sb = (uint32_t)((int64_t)s.tn * BSTRIDE);
     return s;
   };
-  auto issue_stage = [&](const Src& s, int kt, int slot) __attribute__((always_inline)) {
+  // LDS-DMA piece p of a stage (0, 1: A; 2 .. PW - 1: B)
+  auto issue_piece = [&](const Src& s, int kt, int slot, int p) __attribute__((always_inline)) {
     if constexpr ((NQK_PG_DIAG & 4) != 0) return;
-    int8_t* st = lds + slot * PG_STG;
-    if constexpr ((NQK_PG_DIAG & 256) == 0) {  // (diagnostic 256: no A pieces, 128: no B pieces)
-      pg_dma16(r_a, st + (2 * wave) * 1024, va, s.sa + kt * PG_BK);
-      pg_dma16(r_a, st + (2 * wave + 1) * 1024, va, s.sa + 16u * (uint32_t)lda + kt * PG_BK);
+    int8_t* st = lds + slot * STG;
+    if (p < 2) {
+      if constexpr ((NQK_PG_DIAG & 256) == 0)  // (diagnostic 256: no A pieces, 128: no B pieces)
+        pg_dma16(r_a, st + (2 * wave + p) * 1024, va, s.sa + (uint32_t)p * 16u * (uint32_t)lda + kt * PG_BK);
+    } else {
+      if constexpr ((NQK_PG_DIAG & 128) == 0)
+        pg_dma16(r_b, st + PG_ASTG + (NBP * wave + p - 2) * 1024, vb,
+                 s.sb + (uint32_t)(kt * (PG_BN * BROW) + (p - 2) * 1024));
     }
-    if constexpr ((NQK_PG_DIAG & 128) == 0 && !NQK_PG_BREG) {
+  };
+  auto issue_stage = [&](const Src& s, int kt, int slot) __attribute__((always_inline)) {
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-        pg_dma16(r_b, st + PG_ASTG + (4 * wave + p) * 1024, vb, s.sb + (uint32_t)(kt * (PG_BN * PG_BK) + p * 1024));
-    }
+    for (int p = 0; p < PW; ++p) issue_piece(s, kt, slot, p);
   };
   // column constants of a tile (ct[256] | bias[256], 2 KiB): wave w moves bytes
   // [512 w, 512 w + 512) with lanes 0..31 (one VMEM operation per wave, like every wave)
   const rsrc_t r_ct = pg_rsrc(e.colterm, (uint32_t)((uint64_t)N * 4));
   const rsrc_t r_bias = pg_rsrc(e.bias, e.bias ? (uint32_t)((uint64_t)N * 4) : 0u);
   auto issue_colp = [&](int tn, int cslot) __attribute__((always_inline)) {
-    int8_t* dst = lds + PG_COLP + cslot * 2048 + wave * 512;
+    int8_t* dst = lds + COLP + cslot * 2048 + wave * 512;
     const uint32_t voff = (uint32_t)((tn * PG_BN + (wave & 1) * 128 + (lane & 31) * 4) * 4);
     if (lane < 32) {
       if (wave < 2) pg_dma16(r_ct, dst, voff, 0);
@@ -422,29 +432,32 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
 
   v4i acc[8][4];
   v4i a_lo[4], a_hi[4], b0[4], b1[4];
+  v2u p0[4], p1[4];  // B4: the packed fragments of the current / next step (b0 holds the unpacked ones)
   const int8_t* const fa_base = lds + f_off;
-  const int8_t* const fb_base = fa_base + 4096 * wave;
+  const int8_t* const fb_base = B4 ? lds + f_off4 + 2048 * wave : fa_base + 4096 * wave;
   // fragment reads: A subtile i (rows 16 i ..), B subtile j of the wave (rows 64 w + 16 j ..)
   auto rd_a = [&](v4i (&dst)[4], auto SLOT, auto I0, auto Q) __attribute__((always_inline)) {
     if constexpr ((NQK_PG_DIAG & 16) != 0) return;
     constexpr int q = decltype(Q)::value;
-    dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + (decltype(I0)::value + q) * 1024>(fa_base);
+    dst[q] = pg_lds16o<decltype(SLOT)::value * STG + (decltype(I0)::value + q) * 1024>(fa_base);
   };
   auto rd_b = [&](v4i (&dst)[4], auto SLOT, auto Q) __attribute__((always_inline)) {
     if constexpr ((NQK_PG_DIAG & 16) != 0) return;
     constexpr int q = decltype(Q)::value;
-    dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + PG_ASTG + q * 1024>(fb_base);
+    dst[q] = pg_lds16o<decltype(SLOT)::value * STG + PG_ASTG + q * 1024>(fb_base);
   };
-  // BREG: the wave's B fragments of step kt straight into registers: subtile q of the stage
-  // image (the bytes LDS-DMA piece q would have written) at the offset the LDS fragment read
-  // would have used, so every instruction still reads one whole 1 KiB piece
-  const uint32_t vb2 = (uint32_t)(4096 * wave + 64 * l15 + 16 * (lg ^ pg_sw(l15)));
-  auto issue_b = [&](const Src& s, int kt, v4i (&dst)[4]) __attribute__((always_inline)) {
-    if constexpr (NQK_PG_BREG && (NQK_PG_DIAG & 4) == 0) {
+  // B4: 8 nibble bytes per fragment into the packed double buffer; unpack_b expands the
+  // current step's after its wait into b0 (the only unpacked set)
+  auto rd_b4 = [&](v2u (&dst)[4], auto SLOT, auto Q) __attribute__((always_inline)) {
+    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
+    constexpr int q = decltype(Q)::value;
+    dst[q] = pg_lds8o<decltype(SLOT)::value * STG + PG_ASTG + q * 512>(fb_base);
+  };
+  auto unpack_b = [&](const v2u (&p)[4]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[q] = (v4i)pg_load16(r_b, vb2, s.sb + (uint32_t)(kt * (PG_BN * PG_BK) + q * 1024));
-    }
+    for (int q = 0; q < 4; ++q)
+      b0[q] = v4i{(int)((p[q][0] << 4) & 0xF0F0F0F0u), (int)(p[q][0] & 0xF0F0F0F0u), (int)((p[q][1] << 4) & 0xF0F0F0F0u),
+                  (int)(p[q][1] & 0xF0F0F0F0u)};
   };
   // 16 MFMAs of one half step (M-subtiles 4 h .. 4 h + 3) with fn(q) after MFMA q
   auto half = [&](auto H, auto FIRST, const v4i (&aa)[4], const v4i (&bb)[4], const v4i (&ci)[4], auto&& fn)
@@ -468,7 +481,9 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     const int n0 = s.tn * PG_BN;
     const int cw = n0 + 64 * wave;  // the wave's 64 columns: one head, one column group (host)
     const int col0 = cw + 16 * lg;
-    const int8_t* cp = lds + PG_COLP + cslot * 2048;
+    const int8_t* cp = lds + COLP + cslot * 2048;
+    // PG_GLUT: LDS byte address of entry 0 minus bits(GLUT_MAGIC) * 8 (one v_lshl_add per lookup)
+    const uint32_t lut_base = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + LUTO) - (GLUT_MAGIC_BITS << 3);
     float bias[16];
     {
       v4i bb[4];
@@ -531,6 +546,65 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         } else {
           off = (uint32_t)(m * e.ldo + col0);
         }
+        if constexpr (EPI == PG_GLUT) {
+          // GELU by table lookup: h exactly as the reference (F32X), its bucket entry from
+          // the LDS table (one ds_read_b64 per element), the output byte selected by one
+          // compare (nqk_glut.h); no filter and no fallback path
+          float hv[16];
+          uint2 ent[16];
+#pragma unroll
+          for (int q = 0; q < 16; q += 2) {
+            const v4i& av4 = acc[i][q >> 2];
+            const v2f vf = v2f{(float)av4[q & 3], (float)av4[(q & 3) + 1]};
+            const v2f h = v2f{bias[q], bias[q + 1]} + vf * v2f{sacc, sacc};
+            const v2f r = __builtin_elementwise_fma(h, v2f{e.gk.iwR, e.gk.iwR}, v2f{e.gk.cR, e.gk.cR});
+            const v2f l = __builtin_elementwise_fma(h, v2f{e.gk.iwL, e.gk.iwL}, v2f{e.gk.cL, e.gk.cL});
+            hv[q] = h[0];
+            hv[q + 1] = h[1];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const float u = __builtin_amdgcn_fmed3f(__builtin_fmaxf(r[j], l[j]), GLUT_MAGIC, e.gk.uhi);
+              const uint32_t a = (__float_as_uint(u) << 3) + lut_base;
+              const v2u t = *(const __attribute__((address_space(3))) v2u*)(uintptr_t)a;
+              ent[q + j] = make_uint2(t[0], t[1]);
+            }
+          }
+          uint32_t pk[4] = {0, 0, 0, 0};
+          uint64_t slow = 0;  // lanes with an element in its entry's window
+          sfor<0, 16>([&](auto Q) __attribute__((always_inline)) {
+            constexpr int q = decltype(Q)::value;
+            pk[q >> 2] = glut_sel<q & 3>(pk[q >> 2], hv[q], ent[q].x, ent[q].y, slow);
+          });
+          if (__builtin_expect(slow != 0, 0) && (NQK_PG_DIAG & 32) == 0) {
+            // the exact chain for the elements inside a window (wave-uniform branch; a loop
+            // that is not unrolled keeps the chain's code once)
+            // (element q picked by compile-time selects: no runtime-indexed arrays, no scratch)
+#pragma clang loop unroll(disable)
+            for (int q = 0; q < 16; ++q) {
+              float hq = 0.0f;
+              uint32_t tq = 0u, iq = 0u;
+              sfor<0, 16>([&](auto Q) __attribute__((always_inline)) {
+                constexpr int c = decltype(Q)::value;
+                hq = q == c ? hv[c] : hq;
+                tq = q == c ? ent[c].x : tq;
+                iq = q == c ? ent[c].y : iq;
+              });
+              if (glut_in_window(hq, tq, iq)) {
+                const uint32_t qv =
+                    (uint32_t)glut_exact(hq, e.rdiv, e.add1, e.mul2, e.rs_out[0], e.zp_out[0], e.lo, e.hi) & 0xffu;
+                sfor<0, 4>([&](auto G) __attribute__((always_inline)) {
+                  constexpr int g = decltype(G)::value;
+                  const int sh = 8 * (q & 3);
+                  if ((q >> 2) == g) pk[g] = (pk[g] & ~(0xffu << sh)) | (qv << sh);
+                });
+              }
+            }
+          }
+          const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
+          if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
+          else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, off, 0, NQK_PG_STAUX);
+          return;
+        }
         uint32_t pk[4] = {0, 0, 0, 0};
         uint32_t worst = 0;
         uint32_t wgr[4] = {0, 0, 0, 0};  // QKV, GELU4: the measure's maximum per group of 4 elements
@@ -577,8 +651,8 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
             m0 = __builtin_fmaf(__builtin_fabsf(vf[0]), k1, __builtin_fabsf(dd[0]));
             m1 = __builtin_fmaf(__builtin_fabsf(vf[1]), k1, __builtin_fabsf(dd[1]));
             const v2f b = rr + v2f{zp128, zp128};
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[0], 0.0f, 255.0f), q & 3, pk[q >> 2]);
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[1], 0.0f, 255.0f), (q & 3) + 1,
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[0], e.blo, e.bhi), q & 3, pk[q >> 2]);
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[1], e.blo, e.bhi), (q & 3) + 1,
                                                         pk[q >> 2]);
           } else {  // GELU: h exactly as the reference (F32X), then the filtered fast chain
             const v2f h = v2f{bias[q], bias[q + 1]} + vf * v2f{sacc, sacc};
@@ -645,8 +719,8 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   // compiler places their waits (compiler-visible loads).
   const rsrc_t r_res = pg_rsrc(RESID ? e.resid : nullptr, RESID ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
   const rsrc_t r_nul = pg_rsrc(RESID ? e.resid : nullptr, 0u);  // columns past N: loads return 0, stores drop
-  constexpr int TR_ROW = 272;  // bytes per staged row (256 + 16: conflict-free b128 writes)
-  int8_t* const tr = lds + 2 * PG_STG + wave * (16 * TR_ROW);
+  constexpr int TR_ROW = PG_TR_ROW;
+  int8_t* const tr = lds + (B4 ? COLP + 4096 : 2 * STG) + wave * (16 * TR_ROW);
   const int ta = lane & 15, tb = lane >> 4;
   v4u resv[3][4];
   auto res_off = [&](const Src& s, int i, int k) __attribute__((always_inline)) {
@@ -660,7 +734,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
                                  NQK_PG_RLAUX >= 0 ? NQK_PG_RLAUX : (NK == 48 ? 2 : 0));
   };
   auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
-    const int8_t* cp = lds + PG_COLP + cslot * 2048;
+    const int8_t* cp = lds + COLP + cslot * 2048;
     const v4i bb = pg_lds16(cp + 1024 + (64 * wave + 4 * ta) * 4);  // columns 4 a .. 4 a + 3
     const v2f b01 = v2f{__int_as_float(bb[0]), __int_as_float(bb[1])};
     const v2f b23 = v2f{__int_as_float(bb[2]), __int_as_float(bb[3])};
@@ -705,13 +779,11 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   // RESID: 8 x 4 stores after the stages (counted conservatively without the 6 x 4 residual
   // loads, which the compiler may hoist above the stage issues: a smaller count only waits more)
   constexpr int EOPS = RESID ? 32 : 8;
-  // BREG: per stage only the 2 A pieces are LDS-DMA (PWA); the B loads of step kt + 1 are
-  // issued in step kt (before stage kt + 2's A pieces) and waited for by the compiler at
-  // their first use; the next tile's B of step 0 goes out before its A stages
-  constexpr int PWA = NQK_PG_BREG ? 2 : PG_PW;
+  constexpr int PWA = PW;
   Src cur = src_of(tile_at(0));
+  // PG_GLUT: the 4 KiB GELU table into LDS, 1 KiB per wave (waited for with stage 0)
+  if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 0);
   issue_colp(cur.tn, 0);
-  issue_b(cur, 0, b0);
   issue_stage(cur, 0, 0);
   issue_stage(cur, 1, 1);
   if constexpr (NQK_PG_PRIO == 2) {
@@ -733,38 +805,57 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     v4i cinit[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      cinit[j] = pg_lds16(lds + PG_COLP + cs * 2048 + (64 * wave + (RESID ? 16 * j + 4 * lg : 16 * lg + 4 * j)) * 4);
+      cinit[j] = pg_lds16(lds + COLP + cs * 2048 + (64 * wave + (RESID ? 16 * j + 4 * lg : 16 * lg + 4 * j)) * 4);
     sfor<0, 4>([&](auto Q) __attribute__((always_inline)) {
       rd_a(a_lo, ic<0>{}, ic<0>{}, Q);
-      if constexpr (!NQK_PG_BREG) rd_b(b0, ic<0>{}, Q);
+      if constexpr (B4) rd_b4(p0, ic<0>{}, Q);
+      else rd_b(b0, ic<0>{}, Q);
     });
-    if constexpr (NQK_PG_BREG) pg_lgkm_tie(a_lo[0], a_lo[1], a_lo[2], a_lo[3]);
-    else pg_lgkm_tie8(a_lo, b0);
+    if constexpr (B4) {
+      pg_lgkm_tie_a4(a_lo, p0);
+      unpack_b(p0);
+    } else {
+      pg_lgkm_tie8(a_lo, b0);
+    }
     pg_lgkm_tie(cinit[0], cinit[1], cinit[2], cinit[3]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cinit[j] = -cinit[j];
+    for (int j = 0; j < 4; ++j) cinit[j] = B4 ? -(cinit[j] << 4) : -cinit[j];
     sfor<0, NK>([&](auto KT) __attribute__((always_inline)) {
       constexpr int kt = decltype(KT)::value;
       constexpr int slot = kt % PG_RD;
-      v4i(&bc)[4] = (kt & 1) ? b1 : b0;
+      v4i(&bc)[4] = B4 ? b0 : ((kt & 1) ? b1 : b0);
       v4i(&bn)[4] = (kt & 1) ? b0 : b1;
+      v2u(&pc)[4] = (kt & 1) ? p1 : p0;
+      v2u(&pn)[4] = (kt & 1) ? p0 : p1;
       if constexpr (kt > 0) {  // this step's fragments (read in step kt - 1)
-        if constexpr (NQK_PG_BREG) pg_lgkm_tie(a_lo[0], a_lo[1], a_lo[2], a_lo[3]);
-        else pg_lgkm_tie8(a_lo, bc);
+        if constexpr (B4) {
+          pg_lgkm_tie_a4(a_lo, pc);
+          unpack_b(pc);
+        } else {
+          pg_lgkm_tie8(a_lo, bc);
+        }
       }
       // first half: subtiles 0..3; between the MFMAs the second half's A fragments and the
       // refill of the slot step kt - 1 read (stage kt + 2)
       half(ic<0>{}, std::integral_constant<bool, kt == 0>{}, a_lo, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
         constexpr int q = decltype(Q)::value;
         if constexpr (q < 4) rd_a(a_hi, ic<slot>{}, ic<4>{}, Q);
-        if constexpr (q == 2 && NQK_PG_BREG && kt + 1 < NK) issue_b(cur, kt + 1, bn);
-        if constexpr (q == 4 && kt + 2 < NK) issue_stage(cur, kt + 2, (kt + 2) % PG_RD);
+        // stage kt + 2: NQK_PG_SPREAD 0 = all pieces after MFMA 4; 1 = one piece every
+        // other MFMA from MFMA 1 (a burst of LDS-DMA issues costs each piece more:
+        // MI355X_MICROARCH.md, LDS-DMA piece issue cost)
+        if constexpr (kt + 2 < NK) {
+          if constexpr (NQK_PG_SPREAD == 0) {
+            if constexpr (q == 4) issue_stage(cur, kt + 2, (kt + 2) % PG_RD);
+          } else if constexpr ((q & 1) == 1 && (q >> 1) < PW) {
+            issue_piece(cur, kt + 2, (kt + 2) % PG_RD, q >> 1);
+          }
+        }
       });
       if constexpr (kt == 1) issue_colp(nxt.tn, cs ^ 1);
       if constexpr (kt + 1 < NK) {
         // stage kt + 1 landed; younger: stage kt + 2 (if issued), colp (step 1), and for
         // stage 1 the previous tile's epilogue operations
-        constexpr int y = (kt + 2 < NK ? PWA : 0) + ((kt == 1 || kt == 2) ? 1 : 0) + (NQK_PG_BREG ? 4 : 0);
+        constexpr int y = (kt + 2 < NK ? PWA : 0) + ((kt == 1 || kt == 2) ? 1 : 0);
         if (kt == 0 && it > 0) pg_vmcnt<y + EOPS>();
         else pg_vmcnt<y>();
         pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
@@ -777,7 +868,10 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         constexpr int q = decltype(Q)::value;
         if constexpr (kt + 1 < NK) {
           if constexpr (q < 4) rd_a(a_lo, ic<(kt + 1) % PG_RD>{}, ic<0>{}, Q);
-          else if constexpr (q < 8 && !NQK_PG_BREG) rd_b(bn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
+          else if constexpr (q < 8) {
+            if constexpr (B4) rd_b4(pn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
+            else rd_b(bn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
+          }
         }
       });
     });
@@ -787,16 +881,21 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     if constexpr (RESID) {
       res_issue(cur, ic<0>{});
       res_issue(cur, ic<1>{});
-      __builtin_amdgcn_s_barrier();
+      if constexpr (!B4) __builtin_amdgcn_s_barrier();  // (B4: the scratch is not in the ring)
     }
     // (the last tile re-stages its own first stages: never read, drained at the end; the
     // VMEM counts stay the same on every path)
-    issue_b(nxt, 0, b0);
     issue_stage(nxt, 0, 0);
     issue_stage(nxt, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (NQK_PG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(1);
+    if constexpr (B4) {  // the MFMAs accumulated 16 acc
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = acc[i][j] >> 4;
+    }
     if constexpr (RESID) epilogue_resid(cur, cs);
     else epilogue(cur, cs);
     cur = nxt;
@@ -1245,6 +1344,29 @@ __global__ void k_pack_pg(const int8_t* __restrict__ bt, int8_t* __restrict__ ou
   }
 }
 
+// int4 weight image of k_pg<B4> (every value in [-8, 7]): [N / 256][K / 64] stages of 256 rows
+// x 32 B, row rho as in k_pack_pg; an 8-byte chunk c (physical chunk c ^ 2 in rows 8..15 of
+// a 16-row subtile) holds k = 16 c .. 16 c + 15 of the stage as two words h: byte b of word h
+// = k 16 c + 8 h + b in the low nibble, 16 c + 8 h + 4 + b in the high one (the order the
+// kernel's AND masks produce: nqk_fused.hip k_pack_b4)
+__global__ void k_pack_pg4(const int8_t* __restrict__ bt, uint32_t* __restrict__ out, int64_t N, int64_t K,
+                           int64_t ldb, int64_t words, int layout) {
+  const int64_t nk = K / PG_BK;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < words; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t blk = c >> 11, w = c & 2047;  // 2048 words per stage (256 rows x 32 B)
+    const int64_t tn = blk / nk, kt = blk - tn * nk;
+    const int rho = (int)(w >> 3), pc = (int)((w >> 1) & 3), h = (int)(w & 1);
+    const int64_t col = tn * PG_BN + 64 * (rho >> 6) + pg_bperm(rho & 63, layout);
+    const int lc = pc ^ (2 * ((rho >> 3) & 1));
+    uint32_t v = 0;
+    if (col < N) {
+      const int8_t* src = bt + col * ldb + kt * PG_BK + 16 * lc + 8 * h;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) v |= (uint32_t)(((src[b] & 15) | ((src[4 + b] & 15) << 4)) & 0xff) << (8 * b);
+    }
+    out[c] = v;
+  }
+}
 
 }  // namespace
 
@@ -1257,6 +1379,17 @@ extern "C" int nqk_pack_pg(const int8_t* bt, int8_t* out, int64_t N, int64_t K, 
   const int64_t chunks = (N + PG_BN - 1) / PG_BN * PG_BN * K / 16;
   hipLaunchKernelGGL(k_pack_pg, dim3(grid_for(chunks)), dim3(kThreads), 0, stream(), bt, out, N, K, ldb, chunks, layout);
   return launch_status("nqk_pack_pg");
+}
+
+extern "C" int nqk_pack_pg4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t ldb, int layout) {
+  if (N <= 0 || K <= 0) return 0;
+  if (layout != 0 && layout != 1) return fail("nqk_pack_pg4: layout must be 0 (int8 outputs) or 1 (f32 outputs)");
+  if (K % PG_BK) return fail("nqk_pack_pg4: K must be a multiple of 64");
+  if ((((uintptr_t)bt) & 15) || (ldb & 15) || (((uintptr_t)out) & 15)) return fail("nqk_pack_pg4: unaligned operand");
+  const int64_t words = (N + PG_BN - 1) / PG_BN * PG_BN * K / 8;
+  hipLaunchKernelGGL(k_pack_pg4, dim3(grid_for(words)), dim3(kThreads), 0, stream(), bt, (uint32_t*)out, N, K, ldb, words,
+                     layout);
+  return launch_status("nqk_pack_pg4");
 }
 
 static int pg_num_cus() {
@@ -1276,7 +1409,11 @@ static int pg_num_cus() {
 int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, int64_t K, int64_t lda,
               const nqk_epilogue* p, bool f32x) {
   if (getenv("NQK_NO_PG")) return 0;
-  if (bp == nullptr || p->colterm == nullptr || p->b_packed == 2) return 0;
+  if (bp == nullptr || p->colterm == nullptr) return 0;
+  // b_packed == 2: int4 weights; bp is then the nqk_pack_pg4 nibble image (k_pg<B4>)
+  const bool b4 = p->b_packed == 2;
+  if (b4 && !(p->bit_width <= 4 && p->col_absmax > 0 && 16.0 * (double)p->col_absmax * (double)llabs(p->zpa) < 2147483647.0))
+    return 0;
   if (!(epi == PG_QKV || epi == PG_RESID || epi == PG_GELU)) return 0;
   // K = 192 / 768 / 3072 (ViT-Ti / ViT-B widths and MLP), N % 64 == 0 (a partial last column
   // tile: whole waves past N)
@@ -1287,7 +1424,8 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   // tiles of B = 256 fill 77 % of the slots with a quarter of each tile idle, and the
   // one-tile-per-workgroup kernel is faster (29.1 vs 24.9 us, profiles/r03_vit_tiny_pg.txt)
   if (epi == PG_RESID && N % PG_BN != 0) return 0;
-  if (epi == PG_QKV && !(p->hdim == 64 && p->group_cols % 64 == 0 && (double)M * p->heads * p->hdim < 2147483647.0))
+  if (epi == PG_QKV && !(p->hdim == 64 && p->tokens > 0 && p->heads > 0 && p->heads * p->hdim == p->group_cols &&
+                         p->group_cols % 64 == 0 && (double)M * p->heads * p->hdim < 2147483647.0))
     return 0;
   // NQK_PG_NORESID=1 keeps the residual epilogues on k_qgemm_big (the round-2 kernel)
   if (epi == PG_RESID && (getenv("NQK_PG_NORESID") || p->resid == nullptr || (M % PG_BM != 0 && p->resid == p->out[0])))
@@ -1297,7 +1435,11 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   if (!al16(p->out[0]) || !al16(p->out[1]) || !al16(p->out[2]) || !al16(p->resid) || !al16(p->colterm) ||
       !al16(p->bias) || !al16(a) || (lda & 15))
     return 0;
-  if (p->bit_width != 8) return 0;  // the byte clamp by med3 + v_cvt_pk_u8 assumes [-128, 127]
+  // GELU with a table (nqk_gelu_lut_build): the table holds the exact chain's output bytes
+  const bool glut = epi == PG_GELU && p->gelu_lut != nullptr && p->lut_n > 0 && p->lut_n <= GLUT_MAX &&
+                    (((uintptr_t)p->gelu_lut) & 15) == 0 && !getenv("NQK_NO_GLUT");
+  if (p->bit_width < 2 || p->bit_width > 8) return 0;  // int8 outputs
+  const double qlo = -__builtin_ldexp(1.0, p->bit_width - 1), qhi = __builtin_ldexp(1.0, p->bit_width - 1) - 1.0;
   PgEpi e{};
   const int ng = epi == PG_QKV ? 3 : 1;
   for (int g = 0; g < 3; ++g) {
@@ -1311,8 +1453,8 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     e.c1[g] = e.sacc[g] * e.rsf[g];
     e.k1[g] = __builtin_fabsf(e.c1[g]) * 0x1p-21f;
     e.zp128[g] = (float)p->zp_out[gg] + 128.0f;
-    e.qlo[g] = -128.0f - (float)p->zp_out[gg];
-    e.qhi[g] = 127.0f - (float)p->zp_out[gg];
+    e.qlo[g] = (float)qlo - (float)p->zp_out[gg];
+    e.qhi[g] = (float)qhi - (float)p->zp_out[gg];
     e.magic[g] = 0x1.8p23f + (float)p->zp_out[gg];
     e.out[g] = p->out[gg];
     if (epi != PG_RESID) {
@@ -1323,8 +1465,10 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   e.bias = p->bias;
   e.resid = p->resid;
   e.colterm = p->colterm;
-  e.lo = -128.0;
-  e.hi = 127.0;
+  e.lo = qlo;
+  e.hi = qhi;
+  e.blo = (float)qlo + 128.0f;
+  e.bhi = (float)qhi + 128.0f;
   e.group_cols = p->group_cols > 0 ? p->group_cols : (int)N;
   e.tokens = p->tokens;
   e.heads = p->heads;
@@ -1334,6 +1478,8 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   e.add1 = p->add1;
   e.mul2 = p->mul2;
   e.ldo = (int)N;
+  e.lut = glut ? p->gelu_lut : nullptr;
+  e.gk = GLutK{p->lut_k[0], p->lut_k[1], p->lut_k[2], p->lut_k[3], p->lut_k[4]};
   if (epi == PG_GELU) {
     // the GELU filter of nqk_fused.hip make_epi: |gelu_fast - gelu| <= GELU_REL |h| +
     // GELU_ABS, plus the product t = y * rsf
@@ -1348,7 +1494,7 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   // selects k_pg2 (epilogue inside the next tile's k loop, one workgroup per CU), measured
   // slower (its interleaved epilogue does not hide behind the MFMAs)
   const char* kv = getenv("NQK_PG_KERNEL");
-  if (kv && atoi(kv) == 2 && K != 192 && N % PG_BN == 0) {
+  if (kv && atoi(kv) == 2 && K != 192 && N % PG_BN == 0 && !b4 && p->bit_width == 8) {
     const int grid2 = nt < pg_num_cus() ? nt : pg_num_cus();
     const int key2 = epi * 4 + (K == 3072 ? 2 : 0) + (f32x ? 1 : 0);
     switch (key2) {
@@ -1369,36 +1515,35 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   }
   const int slots = 2 * pg_num_cus();
   const int grid = nt < slots ? nt : slots;
-  // initial delay of the second workgroup per CU, in units of s_sleep 8 (~512 cycles)
-  const char* sv = getenv("NQK_PG_STAGGER");
-  const int stg = grid == slots ? (sv ? atoi(sv) : 0) : 0;
-  const char* pv = getenv("NQK_PG_PAIR");
-  const bool pair = K != 192 && (pv ? atoi(pv) != 0 : NQK_PG_PAIR_DEFAULT);
   const int kc = K == 3072 ? 2 : (K == 192 ? 1 : 0);
-  const int key = epi * 16 + kc * 4 + (f32x ? 1 : 0) + (pair ? 2 : 0);
+  const int epi_k = glut ? PG_GLUT : epi;
+  const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0);
   switch (key) {
-#define PGL(E, NKV, X, P)                                                                                       \
-  case E * 16 + (NKV == 48 ? 2 : (NKV == 3 ? 1 : 0)) * 4 + (X ? 1 : 0) + (P ? 2 : 0):                           \
-    hipLaunchKernelGGL((k_pg<E, NKV, X, P>), dim3(P ? (grid + 1) / 2 : grid), dim3(P ? 512 : 256),            \
-                       P ? 2 * PG_LDS : PG_LDS, stream(), a, bp, (int)M, (int)N, (int)lda, tiles_n, nt, stg, e); \
+#define PGL(E, NKV, X, B)                                                                                      \
+  case E * 16 + (NKV == 48 ? 2 : (NKV == 3 ? 1 : 0)) * 4 + (X ? 1 : 0) + (B ? 2 : 0):                          \
+    hipLaunchKernelGGL((k_pg<E, NKV, X, B>), dim3(grid), dim3(256), pg_lds_bytes(E, B), stream(), a, bp, (int)M, \
+                       (int)N, (int)lda, tiles_n, nt, e);                                                      \
     break;
     PGL(PG_QKV, 12, true, false)
     PGL(PG_GELU, 12, true, false)
+    PGL(PG_GLUT, 12, true, false)
     PGL(PG_RESID, 12, true, false) PGL(PG_RESID, 12, false, false) PGL(PG_RESID, 48, true, false)
     PGL(PG_RESID, 48, false, false)
-    PGL(PG_QKV, 12, true, true)
-    PGL(PG_GELU, 12, true, true)
-    PGL(PG_RESID, 12, true, true) PGL(PG_RESID, 12, false, true) PGL(PG_RESID, 48, true, true)
-    PGL(PG_RESID, 48, false, true)
     PGL(PG_QKV, 3, true, false)  // K = 192 (ViT-Ti)
     PGL(PG_GELU, 3, true, false)
+    PGL(PG_GLUT, 3, true, false)
     PGL(PG_RESID, 3, true, false) PGL(PG_RESID, 3, false, false)
+    PGL(PG_QKV, 12, true, true)  // int4 weights (BASELINE configs[4])
+    PGL(PG_GELU, 12, true, true)
+    PGL(PG_GLUT, 12, true, true)
+    PGL(PG_RESID, 12, true, true) PGL(PG_RESID, 12, false, true) PGL(PG_RESID, 48, true, true)
+    PGL(PG_RESID, 48, false, true)
 #undef PGL
     default:
       return 0;
   }
   const int rc = launch_status("nqk_qgemm_fused(pg)");
-  return rc < 0 ? rc : 4;
+  return rc < 0 ? rc : (glut ? 6 : 4);
 }
 
 }  // namespace nqk

@@ -33,7 +33,8 @@ class Epilogue(ctypes.Structure):
                 ("s_acc", ctypes.c_float * 3), ("s_out", ctypes.c_float * 3), ("zp_out", ctypes.c_int64 * 3),
                 ("out", ctypes.c_void_p * 3), ("bias", ctypes.c_void_p), ("resid", ctypes.c_void_p),
                 ("div", ctypes.c_float), ("add1", ctypes.c_float), ("mul2", ctypes.c_float),
-                ("b_packed", ctypes.c_int32), ("colterm", ctypes.c_void_p), ("bt_pg", ctypes.c_void_p)]
+                ("b_packed", ctypes.c_int32), ("colterm", ctypes.c_void_p), ("bt_pg", ctypes.c_void_p),
+                ("gelu_lut", ctypes.c_void_p), ("lut_k", ctypes.c_float * 5), ("lut_n", ctypes.c_int32)]
 
 
 class Attention(ctypes.Structure):
@@ -97,6 +98,10 @@ SIGNATURES = {
     "nqk_pack_pg": [_p, _p, _l, _l, _l, _i],
     "nqk_qgemm_fused": [_i, _p, _p, _l, _l, _l, _l, _l, _l, _lp, _l, _l, ctypes.POINTER(Epilogue)],
     "nqk_qgemm_last_kernel": [],
+    "nqk_pack_pg4": [_p, _p, _l, _l, _l, _i],
+    "nqk_gelu_lut_build": [_f, _l, _i, _f, _f, _f, _p, ctypes.POINTER(_f), ctypes.POINTER(ctypes.c_int32)],
+    "nqk_gelu_lut_check": [_f, _l, _i, _f, _f, _f, _p, ctypes.POINTER(_f), ctypes.c_int32,
+                           ctypes.POINTER(ctypes.c_uint64)],
     "nqk_ln_quant": [_p, _p, _p, _p, _l, _l, _f, _f, _l, _i],
     "nqk_softmax_quant": [_p, _p, _p, _l, _l, _l, _f, _l, _i],
     "nqk_transpose_pad_i8": [_p, _p, _p, _l, _l, _l, _l],

@@ -36,8 +36,13 @@ def _recv_exact(sock: socket.socket, n: int) -> bytes:
     return bytes(buf)
 
 
+_MAX_MSG = 64 << 20  # the largest control message (the blob header is a few hundred KiB)
+
+
 def _recv(sock: socket.socket):
     (n,) = _LEN.unpack(_recv_exact(sock, _LEN.size))
+    if n > _MAX_MSG:
+        raise ConnectionError(f"control plane: message of {n} bytes exceeds the {_MAX_MSG}-byte limit")
     return json.loads(_recv_exact(sock, n))
 
 
@@ -74,9 +79,15 @@ class ControlPlane:
                     conn, _ = srv.accept()
                     conn.settimeout(timeout)
                     conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    r = _recv(conn)["rank"]
-                    if not (0 < r < world) or r in self.peers:
-                        raise ConnectionError(f"control plane: unexpected rank {r}")
+                    try:
+                        hello = _recv(conn)
+                        r = hello["rank"] if isinstance(hello, dict) else None
+                    except (ValueError, KeyError, ConnectionError) as ex:
+                        conn.close()
+                        raise ConnectionError(f"control plane: malformed first message from a peer ({ex})") from ex
+                    if not isinstance(r, int) or not (0 < r < world) or r in self.peers:
+                        conn.close()
+                        raise ConnectionError(f"control plane: unexpected rank {r!r}")
                     self.peers[r] = conn
             finally:
                 srv.close()

@@ -439,14 +439,16 @@ class FusedEmbed:
         hw = ho * wo
         zp = xd.zero_point
         fused_in = (isinstance(xd, QTensor) and xd._bias is None and xd.dev.dtype == np.int8 and h % m.kh == 0 and
-                    w % m.kw == 0 and (zp is None or np.ndim(zp) == 0))
+                    w % m.kw == 0 and (zp is None or (np.ndim(zp) == 0 and abs(int(zp)) <= 1 << 20)))
         if self.posv.size != (hw + 1) * self.kout:
             raise ValueError("position embedding does not match the patch grid")
         eshape = np.asarray(m.expand.inputs[1].data.data).reshape(-1)
         if eshape.size != 3 or int(eshape[0]) != n:
             raise ValueError(f"class-token Expand shape {eshape} does not match the batch {n}")
         out = DeviceArray((n, hw + 1, self.kout), np.float32)
-        folded = fused_in and self.wt is not None and c == 3
+        # (fused_in: the zero point within nqk_patchify_dequant's / nqk_embed_q's 2^20;
+        # nqk_embed_q: at most 65535 row tiles of 128 patches, else the patchify path)
+        folded = fused_in and self.wt is not None and c == 3 and -(-(n * hw) // 128) <= 65535
         if folded:
             cols = None  # nqk_embed_q reads the int8 image itself
         elif fused_in:
@@ -573,8 +575,10 @@ class FusedLayer:
         self.bp = {k: _pack_b(b, self.bw) for k, b in (("qkv", self.bt_qkv), ("o", self.bt_o), ("1", self.bt_1),
                                                         ("2", self.bt_2))}
         # the persistent 16x16x64 GEMM's weight images (nqk_pack_pg; used where it takes the case)
-        self.bpg = {k: _pack_pg(b, self.bw, lay) for k, b, lay in (("qkv", self.bt_qkv, 0), ("o", self.bt_o, 1),
-                                                                    ("1", self.bt_1, 0), ("2", self.bt_2, 1))}
+        # (int4 weights: the nibble image, paired with the big-tile GEMM's nibble pack: b_packed 2)
+        self.bpg = {k: _pack_pg(b, self.bw, lay, nibbles=self.bp[k] is not None and self.bp[k][1] == 2)
+                    for k, b, lay in (("qkv", self.bt_qkv, 0), ("o", self.bt_o, 1), ("1", self.bt_1, 0),
+                                      ("2", self.bt_2, 1))}
         # max |column sum| of each weight: lets the GEMM epilogues prove f32 exactness
         self.cmax = {k: _absmax(c) for k, c in (("qkv", self.col_qkv), ("o", self.col_o), ("1", self.col_1),
                                                  ("2", self.col_2))}
@@ -584,6 +588,9 @@ class FusedLayer:
                                                           ("1", self.col_1, self.p_ln2), ("2", self.col_2, self.p_h))}
         if self.D != m.heads * m.hdim or self.bt_o.shape != (self.D, self.D) or self.bt_2.shape != (self.D, self.F):
             raise NoMatch("layer dimensions")
+        # the FFN-up epilogue's GELU chain + quantize as a table of its output bytes (built and
+        # checked on all finite f32 inputs by nqk_gelu_lut_build; None: the filtered chain)
+        self.glut = _gelu_lut(self.p_h, self.bw, m.gelu_div, m.gelu_add, m.gelu_mul)
         # the one-kernel attention covers head size 64, <= 224 tokens and zero points for
         # which every int32 intermediate is exact (nqk.h); otherwise three launches
         zs = [_zp(self.p_head["q"]), _zp(self.p_head["k"]), _zp(self.p_sm), _zp(self.p_head["v"])]
@@ -717,6 +724,10 @@ class FusedLayer:
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
                       s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[hh.ptr],
                       div=m.gelu_div, add1=m.gelu_add, mul2=m.gelu_mul)
+        if self.glut is not None:
+            e.gelu_lut, e.lut_n = self.glut[0].ptr, self.glut[2]
+            for j, kv in enumerate(self.glut[1]):
+                e.lut_k[j] = kv
         _gemm(EPI_GELU, ln2q, self._b(e, "1", self.bt_1), 1, Mrows, F, D, D, D, None, 0, 0, e)
         # 10) FFN down + bias + residual
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr, col_absmax=self.cmax["2"],
@@ -743,17 +754,40 @@ def _pack_b(bt, bit_width=8):
     return out, 1
 
 
-def _pack_pg(bt, bit_width=8, layout=0):
+def _pack_pg(bt, bit_width=8, layout=0, nibbles=False):
     """The nqk_pack_pg image of a constant Bt [N][K] (int8 weights, K in {192, 768, 3072},
     N % 64 == 0, padded with zero columns to a multiple of 256; layout 0 for the int8-output
-    epilogues QKV / GELU, 1 for the residual epilogues), or None (NQK_NO_PG set, or a shape
-    the persistent 16x16x64 GEMM does not take)."""
+    epilogues QKV / GELU, 1 for the residual epilogues), or with `nibbles` (int4 weights, bit
+    widths <= 4) the nqk_pack_pg4 nibble image, or None (NQK_NO_PG set, or a shape the
+    persistent 16x16x64 GEMM does not take)."""
     N, K = bt.shape
-    if bit_width != 8 or K not in (192, 768, 3072) or N % 64 or os.environ.get("NQK_NO_PG"):
+    if bit_width > 8 or K not in (192, 768, 3072) or N % 64 or os.environ.get("NQK_NO_PG"):
         return None
+    if nibbles:
+        if bit_width > 4:
+            raise ValueError("nibble-packed weights need bit width <= 4")
+        out = DeviceArray(((N + 255) // 256 * 256, K // 2), np.uint8)
+        _lib.call("nqk_pack_pg4", bt.vp, out.vp, N, K, K, layout)
+        return out
     out = DeviceArray(((N + 255) // 256 * 256, K), np.int8)
     _lib.call("nqk_pack_pg", bt.vp, out.vp, N, K, K, layout)
     return out
+
+
+def _gelu_lut(p, bit_width, div, add1, mul2):
+    """(table, bucket coordinate, entries) of the GELU + quantize step function for the FFN-up
+    epilogue (nqk_gelu_lut_build), or None where no exact table exists (then the epilogue runs
+    the filtered chain) or NQK_NO_GLUT is set."""
+    if os.environ.get("NQK_NO_GLUT") or p.zero_point is None:
+        return None
+    lut = DeviceArray((4096,), np.uint8)
+    k = (ctypes.c_float * 5)()
+    n = ctypes.c_int32(0)
+    _lib.call("nqk_gelu_lut_build", _f32(p.scale), int(p.zero_point), int(bit_width), _f32(div), _f32(add1),
+              _f32(mul2), lut.vp, k, ctypes.byref(n))
+    if n.value <= 0:
+        return None
+    return lut, tuple(float(x) for x in k), int(n.value)
 
 
 def _colterm(col, zpa):
@@ -835,6 +869,11 @@ class Workspace:
         return self.bufs
 
 
+class FusedAwayError(AttributeError, RuntimeError):
+    """Reading a FusedAway value.  An AttributeError, so getattr(v, attr, default) and
+    hasattr() probes see a missing attribute instead of an exception."""
+
+
 class FusedAway:
     """The `.data` of a value computed inside a fused step during the last run (it never
     left the step's kernels).  Reading it raises: run with `keep_values = True` to get every
@@ -844,8 +883,8 @@ class FusedAway:
         self.name = name
 
     def __getattr__(self, attr):
-        raise RuntimeError(f"value {self.name!r} was computed inside a fused plan step and not kept; "
-                           "set QModel.keep_values = True to read intermediates")
+        raise FusedAwayError(f"value {self.name!r} was computed inside a fused plan step and not kept; "
+                             "set QModel.keep_values = True to read intermediates")
 
     def __repr__(self):
         return f"FusedAway({self.name!r})"

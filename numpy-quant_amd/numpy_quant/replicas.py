@@ -127,8 +127,10 @@ class ReplicaGroup:
         self.init_device_comm()
         nbytes = 0
         for v in qmodel.values:
+            if v.__class__.__name__ != "Constant":
+                continue
             dev = getattr(getattr(v, "data", None), "dev", None)
-            if v.__class__.__name__ == "Constant" and dev is not None and dev.nbytes:
+            if dev is not None and dev.nbytes:
                 _lib.call("nqk_comm_bcast", dev.vp, dev.nbytes, 0)
                 nbytes += dev.nbytes
         _lib.call("nqk_sync")

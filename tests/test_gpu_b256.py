@@ -83,8 +83,12 @@ def test_vit_b256_int4_matches_batch1_node_loop():
     out = qmodel([x])[0]
     plan = qmodel._plan
     assert plan.fused == 12
-    # the nibble-packed int4 weight images are in use
-    assert all(layer.bp["1"][1] == 2 for kind, layer in plan.steps if kind == "layer")
+    # the nibble-packed int4 weight images are in use, by the persistent 16x16x64 GEMM (k_pg)
+    from numpy_quant import _lib
+    layers = [layer for kind, layer in plan.steps if kind == "layer"]
+    assert all(layer.bp["1"][1] == 2 for layer in layers)
+    assert all(layer.bpg[k] is not None and layer.bpg[k].dtype == np.uint8 for layer in layers for k in layer.bpg)
+    assert _lib.load().nqk_qgemm_last_kernel() == 4  # the last FFN-down GEMM of the forward
     np.testing.assert_array_equal(out, _eager_batch(qmodel, x), err_msg="fused B=256 vs node loop B=256")
     for i, ref in _eager_rows(model, qmodel, x, CHECK).items():
         np.testing.assert_array_equal(out[i], ref, err_msg=f"image {i}")

@@ -1,0 +1,133 @@
+"""The FFN-up epilogue's GELU chain as a table (round 4; nqk_glut.hip, the k_pg PG_GLUT
+epilogue).  The reference chain is model.py Div -> Erf -> Add -> Mul -> Mul on f32
+(numpy_helper.py:95-112 erf) followed by numpy_quantization.py:24-34 quantize.
+
+* nqk_gelu_lut_build derives every entry from the exact chain and checks the whole table on
+  all finite f32 inputs; nqk_gelu_lut_check repeats that check and must find a single altered
+  threshold or output byte;
+* the GEMM with the table epilogue equals the filtered-chain epilogue (itself pinned to the
+  reference through k_qgemm_big, tests/test_gpu_pgemm.py) bit for bit, at the ViT-Base and
+  ViT-Ti shapes, with small output scales that put many values next to rounding boundaries."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SQRT2_F32 = float(np.float32(1.4142135381698608))
+
+
+def _build(s_out, zp, bw=8):
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    lut = DeviceArray((4096,), np.uint8)
+    k = (ctypes.c_float * 5)()
+    n = ctypes.c_int32(-1)
+    _lib.call("nqk_gelu_lut_build", float(np.float32(s_out)), int(zp), bw, SQRT2_F32, 1.0, 0.5, lut.vp, k, ctypes.byref(n))
+    return lut, k, n.value
+
+
+def _check(lut, k, n, s_out, zp, bw=8):
+    from numpy_quant import _lib
+    bad = ctypes.c_uint64(0)
+    _lib.call("nqk_gelu_lut_check", float(np.float32(s_out)), int(zp), bw, SQRT2_F32, 1.0, 0.5, lut.vp, k, n,
+              ctypes.byref(bad))
+    return bad.value
+
+
+# (s_out, zp, bit width): the ViT-Base calibration's GELU outputs (tests/golden/api.json:
+# s ~ 0.0109 .. 0.0124, zp -112 .. -114), the k_pg tests' parameters, other zero points and int4
+CASES = [(0.012436897, -114, 8), (0.010944091, -112, 8), (0.0165, -118, 8), (0.0027, -9, 8), (0.0125, 0, 8),
+         (0.05, -128, 8), (0.2, -7, 4), (0.05, 3, 4), (0.0123, -113, 7)]
+
+
+@pytest.mark.parametrize("s_out,zp,bw", CASES)
+def test_gelu_table_is_exact_on_every_float(s_out, zp, bw):
+    lut, k, n = _build(s_out, zp, bw)
+    if (s_out, zp) == (0.0027, -9):
+        # 0.0027 needs more than 512 buckets: no table, the epilogue keeps the filtered chain
+        assert n == 0
+        return
+    assert 0 < n <= 512, n
+    assert _check(lut, k, n, s_out, zp, bw) == 0
+
+
+def test_gelu_table_check_finds_an_altered_entry():
+    s_out, zp = 0.012436897, -114
+    lut, k, n = _build(s_out, zp)
+    assert n > 0
+    tab = lut.to_host().view(np.uint32).reshape(-1, 2).copy()
+    # the first entry with a threshold: move the threshold by one ulp, then swap its bytes
+    i = int(np.nonzero(tab[:n, 0] != 0x7F800000)[0][n // 8 if n > 8 else 0])
+    for mod in ("ulp", "bytes"):
+        t = tab.copy()
+        if mod == "ulp":
+            t[i, 0] += 1
+        else:
+            t[i, 1] = ((t[i, 1] & 0xFFFF) << 16) | (t[i, 1] >> 16)
+        from numpy_quant.device import DeviceArray
+        alt = DeviceArray.from_host(t.reshape(-1).view(np.uint8))
+        assert _check(alt, k, n, s_out, zp) > 0, mod
+
+
+def test_gelu_table_refuses_other_chains():
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    lut = DeviceArray((4096,), np.uint8)
+    k = (ctypes.c_float * 5)()
+    n = ctypes.c_int32(-1)
+    _lib.call("nqk_gelu_lut_build", 0.0124, -114, 8, 2.0, 1.0, 0.5, lut.vp, k, ctypes.byref(n))
+    assert n.value == 0
+    _lib.call("nqk_gelu_lut_build", 0.0124, -114, 16, SQRT2_F32, 1.0, 0.5, lut.vp, k, ctypes.byref(n))
+    assert n.value == 0
+
+
+def _gelu_gemm(M, N, K, s_out, zp, seed, table, monkeypatch):
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_GELU, _gemm, _pack_b, _pack_pg
+    rng = np.random.default_rng(seed)
+    a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
+    bt_h = rng.integers(-24, 25, size=(N, K), dtype=np.int8)
+    bt = DeviceArray.from_host(bt_h)
+    col_h = bt_h.astype(np.int64).sum(axis=1)
+    col = DeviceArray.from_host(col_h)
+    bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
+    packed, kind = _pack_b(bt, 8)
+    pg = _pack_pg(bt, 8, 0)
+    zpa = -5
+    colterm = DeviceArray.from_host((col_h * zpa).astype(np.int32))
+    for v in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_NO_PG", "NQK_NO_GLUT", "NQK_PG_KERNEL"):
+        monkeypatch.delenv(v, raising=False)
+    e = _lib.Epilogue()
+    e.zp_flags, e.bit_width = _lib.ZP_COL, 8
+    e.zpa, e.col, e.col_absmax = zpa, col.ptr, int(np.abs(col_h).max())
+    e.bias, e.b_packed, e.colterm, e.bt_pg = bias.ptr, kind, colterm.ptr, pg.ptr
+    e.group_cols = 1 << 30
+    out = DeviceArray((M, N), np.int8)
+    out.fill_zero()
+    e.s_acc[0], e.s_out[0], e.zp_out[0], e.out[0] = float(np.float32(1.3e-4)), float(np.float32(s_out)), zp, out.ptr
+    e.div, e.add1, e.mul2 = SQRT2_F32, 1.0, 0.5
+    keep = None
+    if table:
+        lut, k, n = _build(s_out, zp)
+        assert n > 0
+        e.gelu_lut, e.lut_n = lut.ptr, n
+        for j in range(5):
+            e.lut_k[j] = k[j]
+        keep = lut
+    _gemm(EPI_GELU, a, packed, 1, M, N, K, K, K, None, 0, 0, e)
+    del keep
+    return _lib.load().nqk_qgemm_last_kernel(), out.to_host()
+
+
+@pytest.mark.parametrize("M,N,K,s_out,zp", [
+    (128 * 197, 3072, 768, 0.012436897, -114), (300, 3072, 768, 0.0165, -118), (256 * 50, 3072, 768, 0.0125, 0),
+    (128 * 197, 768, 192, 0.012436897, -114), (300, 768, 192, 0.05, -128),
+])
+def test_pg_gelu_table_equals_filtered_chain(M, N, K, s_out, zp, monkeypatch):
+    k0, ref = _gelu_gemm(M, N, K, s_out, zp, M + N, False, monkeypatch)
+    k1, got = _gelu_gemm(M, N, K, s_out, zp, M + N, True, monkeypatch)
+    assert (k0, k1) == (4, 6), (k0, k1)
+    np.testing.assert_array_equal(ref, got)

@@ -17,21 +17,21 @@ def _last_kernel():
     return _lib.load().nqk_qgemm_last_kernel()
 
 
-def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, kernel=2):
+def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, kernel=2, bw=8):
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray
     from numpy_quant.plan import EPI_GELU, EPI_QKV, EPI_RESID, _gemm, _pack_b, _pack_pg
     epi = {"qkv": EPI_QKV, "resid": EPI_RESID, "gelu": EPI_GELU}[epi_name]
     rng = np.random.default_rng(seed)
     a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
-    bt_h = rng.integers(-24, 25, size=(N, K), dtype=np.int8)
+    bt_h = rng.integers(-24, 25, size=(N, K), dtype=np.int8) if bw == 8 else rng.integers(-8, 8, size=(N, K), dtype=np.int8)
     bt = DeviceArray.from_host(bt_h)
     col_h = bt_h.astype(np.int64).sum(axis=1)
     col = DeviceArray.from_host(col_h)
     bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
     resid = DeviceArray.from_host(rng.standard_normal((M, N)).astype(np.float32))
-    packed, kind = _pack_b(bt, 8)
-    pg = _pack_pg(bt, 8, 1 if epi == EPI_RESID else 0)
+    packed, kind = _pack_b(bt, bw)
+    pg = _pack_pg(bt, bw, 1 if epi == EPI_RESID else 0, nibbles=kind == 2)
     assert pg is not None
     zpa = -5
     colterm = DeviceArray.from_host((col_h * zpa).astype(np.int32))
@@ -42,7 +42,7 @@ def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, ker
     if no_f32x:
         monkeypatch.setenv("NQK_NO_F32X", "1")
     e = _lib.Epilogue()
-    e.zp_flags, e.bit_width = _lib.ZP_COL, 8
+    e.zp_flags, e.bit_width = _lib.ZP_COL, bw
     e.zpa, e.col, e.col_absmax = zpa, col.ptr, int(np.abs(col_h).max())
     e.bias, e.b_packed, e.colterm = bias.ptr, kind, colterm.ptr
     e.bt_pg = pg.ptr if use_pg else None
@@ -140,5 +140,23 @@ def test_pg_gemm_vit_tiny_shapes(epi_name, M, N, K, s_out_scale, no_f32x, monkey
         if npref is not None:
             bad = [int((y != r).sum()) for y, r in zip(got, npref)]
             assert bad == [0] * len(npref), bad
+    for x, y in zip(ref, got):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("epi_name,M,N,K,s_out_scale,no_f32x", [
+    ("qkv", 128 * 197, 2304, 768, 1.0, False), ("qkv", 300, 2304, 768, 0.05, False),
+    ("gelu", 128 * 50, 3072, 768, 1.0, False), ("gelu", 300, 3072, 768, 0.1, False),
+    ("resid", 128 * 200, 768, 768, 1.0, False), ("resid", 128 * 197, 768, 3072, 1.0, False),
+    ("resid", 300, 768, 3072, 1.0, True), ("resid", 256 * 197, 768, 3072, 1.0, False),
+])
+def test_pg_gemm_int4_equals_big_tile(epi_name, M, N, K, s_out_scale, no_f32x, monkeypatch):
+    """BASELINE configs[4]: int4 weights as the nqk_pack_pg4 nibble image on k_pg (B operand
+    unpacked after the LDS stage, 16 x the products accumulated, >> 4 in the epilogue), 4-bit
+    output clamps: equal to k_qgemm_big on its own nibble image (nqk_pack_b4), bit for bit."""
+    seed = M + N + K + 4
+    k0, ref, _ = _run(epi_name, M, N, K, s_out_scale, False, no_f32x, monkeypatch, seed, 1, bw=4)
+    k1, got, _ = _run(epi_name, M, N, K, s_out_scale, True, no_f32x, monkeypatch, seed, 1, bw=4)
+    assert (k0, k1) == (1, 4), (k0, k1)
     for x, y in zip(ref, got):
         np.testing.assert_array_equal(x, y)

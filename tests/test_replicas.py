@@ -22,9 +22,23 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _free_ports(n):
+    """n distinct free ports (all sockets held open while probing)."""
+    socks = [socket.socket() for _ in range(n)]
+    try:
+        for s in socks:
+            s.bind(("127.0.0.1", 0))
+        return [s.getsockname()[1] for s in socks]
+    finally:
+        for s in socks:
+            s.close()
+
+
+def _worker(rank, world, port, q, ctrl_port=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    if ctrl_port is not None:  # a separately probed free port (MASTER_PORT + 1 may be taken)
+        os.environ["NQK_CTRL_PORT"] = str(ctrl_port)
     try:
         g = ReplicaGroup()
         calls = []
@@ -62,8 +76,8 @@ def test_replica_control_plane_world2():
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    port, ctrl = _free_ports(2)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, ctrl)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -81,7 +81,16 @@ def setup(name):
     e.bias, e.resid = bias.ptr, resid.ptr
     e.div, e.add1, e.mul2 = float(np.float32(1.4142135381698608)), 1.0, 0.5
     e.b_packed = kind
-    keep = (a, bt0, bt, pg, col, colterm, bias, resid, out, outs)
+    glut = None
+    if epi == 4:  # the GELU table of these output parameters (round 4: the "glut" variant)
+        lut = DeviceArray((4096,), np.uint8)
+        kk = (ctypes.c_float * 5)()
+        nn = ctypes.c_int32(0)
+        _lib.call("nqk_gelu_lut_build", e.s_out[0], e.zp_out[0], 8, e.div, e.add1, e.mul2, lut.vp, kk, ctypes.byref(nn))
+        print(f"  GELU table: {nn.value} entries", flush=True)
+        if nn.value > 0:
+            glut = (lut, kk, nn.value)
+    keep = (a, bt0, bt, pg, col, colterm, bias, resid, out, outs, glut)
     return N, K, epi, a, bt, pg, e, keep
 
 
@@ -125,12 +134,19 @@ for name in sel:
         variants.append((f"pg:{lname}", lib, {}, True))
     for vname, env in envs.items():
         variants.append((f"pg:{vname}", main, env, True))
+    if keep[-1] is not None:
+        variants.append(("glut", main, {}, "glut"))
     variants.append(("pg2", main, {"NQK_PG_KERNEL": "2"}, True))
     variants.append(("r02", main, {"NQK_PROJ_GELU": "1"} if epi == 4 else {}, False))
     res = {v[0]: [] for v in variants}
     for _ in range(ROUNDS):
         for vname, lib, env, use_pg in variants:
             e.bt_pg = pg.ptr if use_pg else None
+            glut = keep[-1] if use_pg == "glut" else None
+            e.gelu_lut, e.lut_n = (glut[0].ptr, glut[2]) if glut else (None, 0)
+            if glut:
+                for j in range(5):
+                    e.lut_k[j] = glut[1][j]
             try:
                 res[vname].append(timed(lib, epi, a, bt, N, K, e, env))
             except RuntimeError as ex:
