@@ -279,7 +279,9 @@ def run_vit(args, group):
     rng = np.random.default_rng(256 + rank)
     x = rng.standard_normal((args.batch, 3, 224, 224)).astype(np.float32)
     x_dev = FTensor(x)  # resident in HBM before timing
-    logits_all = DeviceArray((world, args.batch, 1000), np.float32) if (world > 1 and rank == 0) else None
+    # rank 0's [world, B, 1000] gather target: N > 1, or one rank with NQK_FORCE_COMM=1 (a
+    # 1-rank RCCL communicator: the per-step ncclGather measured on one GPU)
+    logits_all = DeviceArray((world, args.batch, 1000), np.float32) if (group.use_device_comm and rank == 0) else None
     qmodel([x_dev])     # the public call: compiles the fused plan on first use
     plan = qmodel._plan
     log(f"[bench] fused plan: {plan.fused} encoder layers fused, {len(plan.steps)} steps")

@@ -782,7 +782,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   constexpr int PWA = PW;
   Src cur = src_of(tile_at(0));
   // PG_GLUT: the 4 KiB GELU table into LDS, 1 KiB per wave (waited for with stage 0)
-  if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 0);
+  if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
   issue_colp(cur.tn, 0);
   issue_stage(cur, 0, 0);
   issue_stage(cur, 1, 1);

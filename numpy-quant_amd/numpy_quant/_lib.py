@@ -127,6 +127,9 @@ class NQKError(RuntimeError):
 _lib = None
 
 
+_ROUND4 = {"nqk_gelu_lut_build", "nqk_gelu_lut_check", "nqk_pack_pg4"}  # absent from round-3 builds
+
+
 def load() -> ctypes.CDLL:
     """Load libnqk.so once and declare every exported signature."""
     global _lib
@@ -137,7 +140,11 @@ def load() -> ctypes.CDLL:
                        "there is no CPU fallback for the hot path")
     lib = ctypes.CDLL(LIB_PATH)
     for name, args in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if name in _ROUND4:  # a previous round's build (same-box A/B runs, tools/ab.sh)
+                continue
+            raise NQKError(f"libnqk.so lacks {name}: rebuild it (__graft_entry__.build())")
         fn.argtypes = args
         fn.restype = ctypes.c_int
     lib.nqk_last_error.argtypes = []

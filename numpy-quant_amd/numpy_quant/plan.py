@@ -778,7 +778,7 @@ def _gelu_lut(p, bit_width, div, add1, mul2):
     """(table, bucket coordinate, entries) of the GELU + quantize step function for the FFN-up
     epilogue (nqk_gelu_lut_build), or None where no exact table exists (then the epilogue runs
     the filtered chain) or NQK_NO_GLUT is set."""
-    if os.environ.get("NQK_NO_GLUT") or p.zero_point is None:
+    if os.environ.get("NQK_NO_GLUT") or p.zero_point is None or not hasattr(_lib.load(), "nqk_gelu_lut_build"):
         return None
     lut = DeviceArray((4096,), np.uint8)
     k = (ctypes.c_float * 5)()

@@ -8,9 +8,11 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { echo "== $1 rc=$2" >> gpurun_out/probe.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+# pytest: rc 1 = failed tests (recorded, the measurements still run); anything else stops
+tstep() { echo "== $1 rc=$2" >> gpurun_out/probe.status; if [ $2 -ne 0 ] && [ $2 -ne 1 ]; then exit $2; fi; }
 rm -f gpurun_out/probe.status
-timeout -k 10 400 python -u -m pytest tests/test_gpu_glut.py "tests/test_gpu_pgemm.py::test_pg_gemm_int4_equals_big_tile" tests/test_gpu_b256.py -x -v --timeout 200 --timeout-method thread > gpurun_out/glut_tests.log 2>&1
-step glut_tests $?
+timeout -k 10 400 python -u -m pytest tests/test_gpu_glut.py "tests/test_gpu_pgemm.py::test_pg_gemm_int4_equals_big_tile" tests/test_gpu_b256.py -v --timeout 200 --timeout-method thread > gpurun_out/glut_tests.log 2>&1
+tstep glut_tests $?
 PGM_LIBS=spread=tools/diag/libnqk_spread.so PGM_ROUNDS=3 timeout -k 10 300 python -u tools/pg_micro.py > gpurun_out/pg_micro.txt 2>&1
 step pg_micro $?
 for m in fill xwave valu overlap2; do
