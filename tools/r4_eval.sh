@@ -16,7 +16,7 @@ fi
 timeout -k 10 400 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 step bench $?
 if [ "${SKIP_AB:-0}" != "1" ]; then
-  AB_LIBS="main r3" AB_ENVS="comm:NQK_FORCE_COMM=1 noglut:NQK_NO_GLUT=1" AB_REPS=1 OUT=r4 bash tools/ab.sh
+  AB_LIBS="main r3" AB_ENVS="comm:NQK_FORCE_COMM=1 noglut:NQK_NO_GLUT=1 lnexact:NQK_LN_EXACTQ=1" AB_REPS=1 OUT=r4 bash tools/ab.sh
   step ab $?
 fi
 SKIP_TESTS=1 SKIP_BENCH=1 bash tools/gpu_full.sh
