@@ -30,6 +30,15 @@
 #ifndef NQK_ATTN_PK
 #define NQK_ATTN_PK 1  // FAST path on element pairs with packed f32 arithmetic (0: scalar, for A/B)
 #endif
+#ifndef NQK_ATTN_ROT
+#define NQK_ATTN_ROT 0  // 1: the wave holding one row tile instead of two rotates with blockIdx
+#endif
+#ifndef NQK_ATTN_PQ2
+#define NQK_ATTN_PQ2 0  // 1: P quantize without the clamp when no row can reach it, by fma rounding
+#endif
+#ifndef NQK_ATTN_CTXPK
+#define NQK_ATTN_CTXPK 0  // 1: context quantize on element pairs (round_magic2 + one filter measure)
+#endif
 
 namespace nqk {
 namespace {
@@ -200,7 +209,10 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   const int gt0 = g0_0 + ng0, gt1 = g0_1 + ng1;  // tail groups
 
   const int r32 = lane & 31, h = lane >> 5;
-  for (int rt = wave; rt < NT; rt += 4) {
+  // NT = 7 row tiles on 4 waves: waves (3 + rot) % 4 hold one tile, the others two; rot from
+  // blockIdx spreads the light wave over the SIMDs (NQK_ATTN_ROT)
+  const int rot = NQK_ATTN_ROT ? ((bh ^ (bh >> 3) ^ (bh >> 6)) & 3) : 0;
+  for (int rt = (wave + rot) & 3; rt < NT; rt += 4) {
     const int m0 = rt * 32, m = m0 + r32;
     v4i qb[2];
     {
@@ -354,6 +366,13 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     // then at once its share of O^T = V^T P^T (B operand = P row m, 16 consecutive tokens
     // per half), so only one tile's packed P is live
     int rp = 0;
+    // NQK_ATTN_PQ2: when every lane's kpf <= pqhi (and pqlo <= 0), e kpf in [0, kpf] never
+    // reaches a clamp (wave-uniform): s = RN(e kpf + pmagic) is rint(e kpf) + pmagic from
+    // the exact product (one rounding fewer than tf = RN(e kpf), so still within |t| 2^-22 of
+    // t), dd = RN(e kpf - (s - pmagic)) within 2^-25 of the exact distance (the limit takes
+    // 2^-24 off for it)
+    const bool pq_nc = NQK_ATTN_PQ2 && pqlo <= 0.0f && __all(kpf <= pqhi);
+    const float plim2 = plim - 0x1p-24f;
     v16i acc2[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -372,6 +391,47 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         // one v_max per element; a tile with any element at or past plim recomputes the
         // same tf per element and sends those elements through the exact chain
         float worst = 0.0f;
+        if (NQK_ATTN_PQ2 && NQK_ATTN_PK && pq_nc) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            if (pad_group(c, qq)) {
+              dw[qq] = 0;
+              continue;
+            }
+            const v2f_t k2 = v2f_t{kpf, kpf}, m2 = v2f_t{pmagic, pmagic};
+            const v2f_t e0 = v2f_t{e[c][4 * qq], e[c][4 * qq + 1]}, e1 = v2f_t{e[c][4 * qq + 2], e[c][4 * qq + 3]};
+            const v2f_t s0 = __builtin_elementwise_fma(e0, k2, m2), s1 = __builtin_elementwise_fma(e1, k2, m2);
+            const v2f_t dd0 = __builtin_elementwise_fma(e0, k2, -(s0 - m2));
+            const v2f_t dd1 = __builtin_elementwise_fma(e1, k2, -(s1 - m2));
+            worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd0[0]), __builtin_fabsf(dd0[1])));
+            worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd1[0]), __builtin_fabsf(dd1[1])));
+            uint32_t w = pack4_low(s0, s1);
+            if (!(TC > 0 && c * 32 + 8 * qq + 8 <= TC)) {  // padded columns: 0
+              const int n = c * 32 + 8 * qq + 4 * h;
+              uint32_t keep = 0;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) keep |= (n + j < T ? 0xffu : 0u) << (8 * j);
+              w &= keep;
+            }
+            dw[qq] = (int)w;
+          }
+          if (__builtin_expect(__any(!(worst < plim2)), 0)) {
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+              if (pad_group(c, qq)) continue;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int n = c * 32 + 8 * qq + 4 * h + j;
+                const float x = e[c][4 * qq + j];
+                const float d = __builtin_fmaf(x, kpf, -((__builtin_fmaf(x, kpf, pmagic)) - pmagic));
+                if (!(__builtin_fabsf(d) < plim2)) {
+                  const int qv = n < T ? quant_w(div_rc_w(x, rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) : 0;
+                  dw[qq] = (int)(((uint32_t)dw[qq] & ~(0xffu << (8 * j))) | ((uint32_t)(qv & 0xff) << (8 * j)));
+                }
+              }
+            }
+          }
+        } else {
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           if (pad_group(c, qq)) {
@@ -425,6 +485,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
               }
             }
           }
+        }
         }
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq)
@@ -492,6 +553,32 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         if constexpr ((NQK_ATTN_DIAG & 16) != 0) {  // (diagnostic 16: context bytes without the quantize)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) qs[jj] = (int)o[jj];
+        } else if constexpr (FAST && NQK_ATTN_CTXPK) {
+          // pairs: tf = o rs (one v_pk_mul), clamp + magic-number rounding (round_magic2), the
+          // measure |tf| 2^-21 + |dd| of the four elements against the limit of quant_filter
+          v2f_t dd0, dd1;
+          const v2f_t t0 = v2f_t{o[0], o[1]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
+          const v2f_t t1 = v2f_t{o[2], o[3]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
+          const v2f_t s0 = round_magic2(t0, a.lo_f - a.zp_ctx_f, a.hi_f - a.zp_ctx_f, 0x1.8p23f + a.zp_ctx_f, dd0);
+          const v2f_t s1 = round_magic2(t1, a.lo_f - a.zp_ctx_f, a.hi_f - a.zp_ctx_f, 0x1.8p23f + a.zp_ctx_f, dd1);
+          const float m0 = __builtin_fmaf(__builtin_fabsf(t0[0]), 0x1p-21f, __builtin_fabsf(dd0[0]));
+          const float m1 = __builtin_fmaf(__builtin_fabsf(t0[1]), 0x1p-21f, __builtin_fabsf(dd0[1]));
+          const float m2 = __builtin_fmaf(__builtin_fabsf(t1[0]), 0x1p-21f, __builtin_fabsf(dd1[0]));
+          const float m3 = __builtin_fmaf(__builtin_fabsf(t1[1]), 0x1p-21f, __builtin_fabsf(dd1[1]));
+          // NaN / inf order above every finite measure as unsigned bits
+          const uint32_t wm = __builtin_elementwise_max(__builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)),
+                                                        __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3)));
+          packed = pack4_low(s0, s1);
+          if (__builtin_expect(__any(wm >= __float_as_uint(0x1.fffffcp-2f)), 0)) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int qv = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
+              packed = (packed & ~(0xffu << (8 * jj))) | ((uint32_t)(qv & 0xff) << (8 * jj));
+            }
+          }
+          if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
+          __builtin_amdgcn_sched_barrier(0);
+          continue;
         } else if constexpr (FAST) {
           bool sl[4];
 #pragma unroll

@@ -1514,33 +1514,60 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     return rc2 < 0 ? rc2 : 5;
   }
   const int slots = 2 * pg_num_cus();
-  const int grid = nt < slots ? nt : slots;
   const int kc = K == 3072 ? 2 : (K == 192 ? 1 : 0);
   const int epi_k = glut ? PG_GLUT : epi;
   const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0);
-  switch (key) {
+  auto launch = [&](const int8_t* a_, int m_, int ntiles_, int grid_, const PgEpi& e_) {
+    switch (key) {
 #define PGL(E, NKV, X, B)                                                                                      \
   case E * 16 + (NKV == 48 ? 2 : (NKV == 3 ? 1 : 0)) * 4 + (X ? 1 : 0) + (B ? 2 : 0):                          \
-    hipLaunchKernelGGL((k_pg<E, NKV, X, B>), dim3(grid), dim3(256), pg_lds_bytes(E, B), stream(), a, bp, (int)M, \
-                       (int)N, (int)lda, tiles_n, nt, e);                                                      \
-    break;
-    PGL(PG_QKV, 12, true, false)
-    PGL(PG_GELU, 12, true, false)
-    PGL(PG_GLUT, 12, true, false)
-    PGL(PG_RESID, 12, true, false) PGL(PG_RESID, 12, false, false) PGL(PG_RESID, 48, true, false)
-    PGL(PG_RESID, 48, false, false)
-    PGL(PG_QKV, 3, true, false)  // K = 192 (ViT-Ti)
-    PGL(PG_GELU, 3, true, false)
-    PGL(PG_GLUT, 3, true, false)
-    PGL(PG_RESID, 3, true, false) PGL(PG_RESID, 3, false, false)
-    PGL(PG_QKV, 12, true, true)  // int4 weights (BASELINE configs[4])
-    PGL(PG_GELU, 12, true, true)
-    PGL(PG_GLUT, 12, true, true)
-    PGL(PG_RESID, 12, true, true) PGL(PG_RESID, 12, false, true) PGL(PG_RESID, 48, true, true)
-    PGL(PG_RESID, 48, false, true)
+    hipLaunchKernelGGL((k_pg<E, NKV, X, B>), dim3(grid_), dim3(256), pg_lds_bytes(E, B), stream(), a_, bp, m_,  \
+                       (int)N, (int)lda, tiles_n, ntiles_, e_);                                                \
+    return true;
+      PGL(PG_QKV, 12, true, false)
+      PGL(PG_GELU, 12, true, false)
+      PGL(PG_GLUT, 12, true, false)
+      PGL(PG_RESID, 12, true, false) PGL(PG_RESID, 12, false, false) PGL(PG_RESID, 48, true, false)
+      PGL(PG_RESID, 48, false, false)
+      PGL(PG_QKV, 3, true, false)  // K = 192 (ViT-Ti)
+      PGL(PG_GELU, 3, true, false)
+      PGL(PG_GLUT, 3, true, false)
+      PGL(PG_RESID, 3, true, false) PGL(PG_RESID, 3, false, false)
+      PGL(PG_QKV, 12, true, true)  // int4 weights (BASELINE configs[4])
+      PGL(PG_GELU, 12, true, true)
+      PGL(PG_GLUT, 12, true, true)
+      PGL(PG_RESID, 12, true, true) PGL(PG_RESID, 12, false, true) PGL(PG_RESID, 48, true, true)
+      PGL(PG_RESID, 48, false, true)
 #undef PGL
-    default:
-      return 0;
+      default:
+        return false;
+    }
+  };
+  // Tail split: the static schedule runs ceil(nt / slots) rounds; when the last round is at
+  // most half full (N = 768 at B = 256: 1182 tiles = 2.31 rounds on 512 slots) the rows of
+  // the whole rounds go to one launch and the remaining row panels to a second one with one
+  // workgroup per tile, fewer than there are CUs, so each runs alone on its CU (both MFMA
+  // pipes' shares of its SIMDs, no second workgroup's barriers).  Not for QKV (its head
+  // layout addresses rows by image).  NQK_PG_SPLIT=0 disables it.
+  const int rounds = nt / slots, rem = nt - rounds * slots;
+  const char* sv = getenv("NQK_PG_SPLIT");
+  const bool split = !(sv && atoi(sv) == 0) && epi != PG_QKV && rounds >= 1 && rem > 0 && rem <= slots / 2 &&
+                     (int64_t)(rounds * slots / tiles_n) * PG_BM <= M - PG_BM;
+  if (split) {
+    const int p1 = rounds * slots / tiles_n;  // whole row panels of the main launch
+    const int64_t m1 = (int64_t)p1 * PG_BM, m2 = M - m1;
+    const int nt1 = p1 * tiles_n, nt2 = (int)((m2 + PG_BM - 1) / PG_BM) * tiles_n;
+    PgEpi e2 = e;
+    const size_t osz = epi == PG_RESID ? 4 : 1;
+    e2.out[0] = (char*)e.out[0] + (size_t)m1 * N * osz;
+    e2.out[1] = e2.out[2] = e2.out[0];
+    if (epi == PG_RESID) e2.resid = e.resid + (size_t)m1 * N;
+    if (!launch(a, (int)m1, nt1, nt1 < slots ? nt1 : slots, e)) return 0;
+    const int rc1 = launch_status("nqk_qgemm_fused(pg)");
+    if (rc1 < 0) return rc1;
+    if (!launch(a + m1 * lda, (int)m2, nt2, nt2 < slots ? nt2 : slots, e2)) return 0;
+  } else {
+    if (!launch(a, (int)M, nt, nt < slots ? nt : slots, e)) return 0;
   }
   const int rc = launch_status("nqk_qgemm_fused(pg)");
   return rc < 0 ? rc : (glut ? 6 : 4);

@@ -19,6 +19,13 @@ if [ "${SKIP_AB:-0}" != "1" ]; then
   AB_LIBS="main r3" AB_ENVS="comm:NQK_FORCE_COMM=1 noglut:NQK_NO_GLUT=1 lnexact:NQK_LN_EXACTQ=1" AB_REPS=1 OUT=r4 bash tools/ab.sh
   step ab $?
 fi
+# tail split of the N = 768 GEMMs (pg_launch) and the attention variants (diagnostic builds)
+timeout -k 10 300 env PGM_SHAPES=out,up,down PGM_ENV="nosplit:NQK_PG_SPLIT=0" python -u tools/pg_micro.py \
+  > gpurun_out/r4_pg_split.txt 2>&1
+step pg_split $?
+timeout -k 10 300 env AM_LIBS=arot=tools/diag/libnqk_arot.so,acpk=tools/diag/libnqk_acpk.so,apq=tools/diag/libnqk_apq.so,apc=tools/diag/libnqk_apc.so,aboth=tools/diag/libnqk_aboth.so \
+  python -u tools/attn_micro.py > gpurun_out/r4_attn_ab.txt 2>&1
+step attn_ab $?
 SKIP_TESTS=1 SKIP_BENCH=1 bash tools/gpu_full.sh
 step gpu_full $?
 echo done >> gpurun_out/full.status
