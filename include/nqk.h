@@ -336,8 +336,9 @@ int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_t* v, int8_
  * reference's erf (used by the fused kernels) with the IEEE-division ones on all 2^32
  * float inputs; adds the mismatch counts to counts_dev[0] (exp) / [1] (erf), and those of
  * the attention kernel's non-positive-argument exp against NumPy's exp to [2] and of its
- * packed two-lane variant to [3] (all 2^31 inputs x <= 0).  counts_dev and examples_dev
- * hold 4 entries each. */
+ * packed two-lane variant to [3] (all 2^31 inputs x <= 0), and of the exponent-add variant
+ * for softmax rows with arguments in [-86.5, 0] to [4].  counts_dev and examples_dev hold 5
+ * entries each. */
 int nqk_selftest_fastmath(unsigned long long* counts_dev, uint32_t* examples_dev);
 /* Diagnostic: checks the error bound of the GELU filter's cheap approximation on all
  * 2^32 inputs; stats_dev[0] = violations, [1] = an example, [2 + e] = max error per

@@ -30,14 +30,14 @@
 #ifndef NQK_ATTN_PK
 #define NQK_ATTN_PK 1  // FAST path on element pairs with packed f32 arithmetic (0: scalar, for A/B)
 #endif
-#ifndef NQK_ATTN_ROT
-#define NQK_ATTN_ROT 0  // 1: the wave holding one row tile instead of two rotates with blockIdx
-#endif
 #ifndef NQK_ATTN_PQ2
-#define NQK_ATTN_PQ2 0  // 1: P quantize without the clamp when no row can reach it, by fma rounding
+#define NQK_ATTN_PQ2 1  // 1: P quantize without the clamp when no row can reach it, by fma rounding
 #endif
-#ifndef NQK_ATTN_CTXPK
-#define NQK_ATTN_CTXPK 0  // 1: context quantize on element pairs (round_magic2 + one filter measure)
+#ifndef NQK_ATTN_EXP2
+#define NQK_ATTN_EXP2 1  // 1: rows whose arguments all lie in [-86.5, 0] take np_expf_safe2
+#endif
+#ifndef NQK_ATTN_PSUM
+#define NQK_ATTN_PSUM 1  // 1: the pairwise-sum accumulators as packed pairs (v_pk_add_f32)
 #endif
 
 namespace nqk {
@@ -55,16 +55,6 @@ struct AttnArgs {
   float inv_div, rs_ctx_f, zp_p_f, zp_ctx_f, lo_f, hi_f;  // FAST path constants
   float s_qkd;  // s_qk / div (div a power of two, s_qk / div in [2^-100, 2^100]: exact)
 };
-
-// rint(zp + t) for t approximated by tf with |t - tf| <= |tf| * 2^-21: decided by tf when
-// the boundary is farther than that (zp is an integer, so zp + t rounds like t away from
-// ties); else *slow is set and the caller recomputes exactly
-__device__ __forceinline__ int quant_filter(float tf, float zpf, float lof, float hif, bool* slow) {
-  const float r = __builtin_rintf(tf);
-  const float room = 0.5f - __builtin_fabsf(tf - r);
-  *slow = !(room > __builtin_fabsf(tf) * 0x1p-21f + 0x1p-126f);
-  return (int)__builtin_amdgcn_fmed3f(r + zpf, lof, hif);  // r finite here unless *slow
-}
 
 __device__ __forceinline__ int swz64a(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
@@ -209,10 +199,9 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   const int gt0 = g0_0 + ng0, gt1 = g0_1 + ng1;  // tail groups
 
   const int r32 = lane & 31, h = lane >> 5;
-  // NT = 7 row tiles on 4 waves: waves (3 + rot) % 4 hold one tile, the others two; rot from
-  // blockIdx spreads the light wave over the SIMDs (NQK_ATTN_ROT)
-  const int rot = NQK_ATTN_ROT ? ((bh ^ (bh >> 3) ^ (bh >> 6)) & 3) : 0;
-  for (int rt = (wave + rot) & 3; rt < NT; rt += 4) {
+  // (NT = 7 row tiles on 4 waves: wave 3 holds one.  Rotating that light wave over the
+  // waves by blockIdx measured 2 % slower, profiles/r04_attn_variants_ab.txt)
+  for (int rt = wave; rt < NT; rt += 4) {
     const int m0 = rt * 32, m = m0 + r32;
     v4i qb[2];
     {
@@ -227,6 +216,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     // max; only one tile's accumulators are live
     float e[NT][16];
     float mx = -__builtin_inff();
+    float mn = __builtin_inff();  // NQK_ATTN_EXP2: the smallest score of the whole groups
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
       // the accumulators start at -(row term + column term): the MFMAs then leave the
@@ -267,6 +257,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             e[c][r] = y[0];
             e[c][r + 1] = y[1];
             mx = __builtin_fmaxf(mx, __builtin_fmaxf(y[0], y[1]));
+            if (NQK_ATTN_EXP2 && full) mn = __builtin_fminf(mn, __builtin_fminf(y[0], y[1]));
           }
           __builtin_amdgcn_sched_barrier(0);
           continue;
@@ -292,7 +283,34 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
       mx = o > mx ? o : mx;
     }
     const float nm = -mx;
-    if constexpr (FAST && NQK_ATTN_PK && (NQK_ATTN_DIAG & 2) == 0) {
+    // NQK_ATTN_EXP2: every argument y - max of the whole groups in [-86.5, 0] in all lanes
+    // (RN(mn - mx) is the smallest; straddling groups keep np_expf_nonpos2 for their -inf pads)
+    const bool esafe = NQK_ATTN_EXP2 && __all(mn + nm >= NP_EXP_SAFE_LO);
+    if (FAST && NQK_ATTN_PK && NQK_ATTN_EXP2 && TC > 0 && (NQK_ATTN_DIAG & 2) == 0) {
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        if (esafe) {
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            if (pad_group(c, r >> 2)) continue;  // stays 0
+            const v2f_t xa = v2f_t{e[c][r], e[c][r + 1]} + v2f_t{nm, nm};
+            const v2f_t x = (TC > 0 && c * 32 + 8 * (r >> 2) + 8 <= TC) ? np_expf_safe2(xa) : np_expf_nonpos2(xa);
+            e[c][r] = x[0];
+            e[c][r + 1] = x[1];
+            if ((r % NQK_ATTN_EXPW) == NQK_ATTN_EXPW - 2) __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            if (pad_group(c, r >> 2)) continue;  // stays 0
+            const v2f_t x = np_expf_nonpos2(v2f_t{e[c][r], e[c][r + 1]} + v2f_t{nm, nm});
+            e[c][r] = x[0];
+            e[c][r + 1] = x[1];
+            if ((r % NQK_ATTN_EXPW) == NQK_ATTN_EXPW - 2) __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    } else if constexpr (FAST && NQK_ATTN_PK && (NQK_ATTN_DIAG & 2) == 0) {
 #pragma unroll
       for (int c = 0; c < NT; ++c)
 #pragma unroll
@@ -318,6 +336,42 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     float ra[2][4], tv[2][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) ra[0][j] = ra[1][j] = tv[0][j] = tv[1][j] = 0.0f;
+    if constexpr (NQK_ATTN_PSUM && TC > 0) {
+      // accumulators j, j + 1 as one packed pair: per lane the same IEEE adds in the same order
+      v2f_t pa[2][2], pt[2][2];
+#pragma unroll
+      for (int l = 0; l < 2; ++l) pa[l][0] = pa[l][1] = pt[l][0] = pt[l][1] = v2f_t{0.0f, 0.0f};
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int c = g >> 2, qq = g & 3;
+        const bool f0 = g == g0_0, in0 = g < g0_0 + ng0;
+        const bool f1 = g == g0_1, in1 = g >= g0_1 && g < g0_1 + ng1;
+        const v2f_t x01 = v2f_t{e[c][4 * qq], e[c][4 * qq + 1]}, x23 = v2f_t{e[c][4 * qq + 2], e[c][4 * qq + 3]};
+        if (in0) {
+          pa[0][0] = f0 ? x01 : pa[0][0] + x01;
+          pa[0][1] = f0 ? x23 : pa[0][1] + x23;
+        }
+        if (in1) {
+          pa[1][0] = f1 ? x01 : pa[1][0] + x01;
+          pa[1][1] = f1 ? x23 : pa[1][1] + x23;
+        }
+        if (g == gt0) {
+          pt[0][0] = x01;
+          pt[0][1] = x23;
+        }
+        if (g == gt1) {
+          pt[1][0] = x01;
+          pt[1][1] = x23;
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < 2; ++l)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ra[l][j] = pa[l][j >> 1][j & 1];
+          tv[l][j] = pt[l][j >> 1][j & 1];
+        }
+    } else
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int c = g >> 2, qq = g & 3;
@@ -553,9 +607,11 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         if constexpr ((NQK_ATTN_DIAG & 16) != 0) {  // (diagnostic 16: context bytes without the quantize)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) qs[jj] = (int)o[jj];
-        } else if constexpr (FAST && NQK_ATTN_CTXPK) {
-          // pairs: tf = o rs (one v_pk_mul), clamp + magic-number rounding (round_magic2), the
-          // measure |tf| 2^-21 + |dd| of the four elements against the limit of quant_filter
+        } else if constexpr (FAST) {
+          // rint(zp + t) for t = RN(o / s_ctx) approximated by tf = o rs (|t - tf| <= |tf| 2^-21),
+          // on pairs: one v_pk_mul, clamp + magic-number rounding (round_magic2), and the
+          // measure |tf| 2^-21 + |dd| of the four elements: below 0.5 - 2^-23 every element's
+          // rounding boundary is farther than the error, else the exact chain (quant_w)
           v2f_t dd0, dd1;
           const v2f_t t0 = v2f_t{o[0], o[1]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
           const v2f_t t1 = v2f_t{o[2], o[3]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
@@ -579,15 +635,6 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
           __builtin_amdgcn_sched_barrier(0);
           continue;
-        } else if constexpr (FAST) {
-          bool sl[4];
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) qs[jj] = quant_filter(o[jj] * a.rs_ctx_f, a.zp_ctx_f, a.lo_f, a.hi_f, &sl[jj]);
-          if (__builtin_expect(__any(sl[0] | sl[1] | sl[2] | sl[3]), 0)) {
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj)
-              if (sl[jj]) qs[jj] = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
-          }
         } else {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) qs[jj] = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);

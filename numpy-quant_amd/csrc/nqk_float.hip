@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(256) k_minmax_final(const float* __restrict__ 
 // np_expf; ex[k] = an example
 __global__ void k_fastmath_check(unsigned long long* counts, uint32_t* ex) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  unsigned long long ce = 0, cr = 0, cn = 0, cp = 0;
+  unsigned long long ce = 0, cr = 0, cn = 0, cp = 0, cs = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t(1) << 32); i += stride) {
     const float x = __uint_as_float((uint32_t)i);
     const float a = np_expf_t<true>(x), b = np_expf_t<false>(x);
@@ -270,11 +270,19 @@ __global__ void k_fastmath_check(unsigned long long* counts, uint32_t* ex) {
         ex[3] = (uint32_t)i;
       }
     }
+    if (x <= 0.0f && x >= NP_EXP_SAFE_LO) {
+      const v2f_t p = np_expf_safe2(v2f_t{x, x});
+      if (__float_as_uint(p[0]) != __float_as_uint(b) || __float_as_uint(p[1]) != __float_as_uint(b)) {
+        ++cs;
+        ex[4] = (uint32_t)i;
+      }
+    }
   }
   if (ce) atomicAdd(counts, ce);
   if (cr) atomicAdd(counts + 1, cr);
   if (cn) atomicAdd(counts + 2, cn);
   if (cp) atomicAdd(counts + 3, cp);
+  if (cs) atomicAdd(counts + 4, cs);
 }
 
 // exhaustive check of the GELU filter bound (nqk_numerics.h gelu_fast) for the graph

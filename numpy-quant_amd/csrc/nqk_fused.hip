@@ -1596,16 +1596,14 @@ k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const f
 // 96-column leaf: conflict-free reads in the tree layout), read in the tree layout,
 // and the packed int8 results written back into LDS (784-B rows: conflict-free dword
 // writes) and stored linearly.  No workgroup barrier: each wave owns its LDS image.
-// FQ: the quantize through a rounding filter in f32 (round 4): tf = RN(y RN32(1 / s)) is within
-// |t| 2^-22 of t = RN32(y / s), so where tf lies farther than |tf| 2^-21 from a rounding
-// boundary rint(zp + t) = zp + rint(tf) (zp an integer, |zp| <= 2^20: exact in f32); a group
-// of 4 elements per lane with any element nearer than that takes the exact f64 chain
-// (wave-uniform branch, ~1 % of the groups).  The f64 chain costs ~2.5x the filter's VALU.
-template <int NL, bool FQ>
+// (An f32 rounding filter in front of the f64 quantize chain measured slower here: 40.9 vs
+// 39.3 us per launch at 50432 x 768, profiles/r04_ln_filter_dropped.txt — the kernel is bound
+// by its loads and stores, not by the quantize.)
+template <int NL>
 __global__ void __launch_bounds__(256)
 k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
                int8_t* __restrict__ out, int64_t rows, float eps, float s, double rs, double zp, double lo,
-               double hi, float rsf, float zp128, float lo128, float hi128) {
+               double hi) {
   constexpr int LF = 96, LPR = NL * 2, NI = LF / 8, COLS = NL * LF, RW = 64 / LPR;
   constexpr int CH = COLS / 4;                      // 16-B chunks per row
   constexpr int RSI = COLS * 4 + NL * 16;           // LDS bytes per input row
@@ -1675,30 +1673,12 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
     const float y[4] = {((xv[i].x * inv) * gg.x) + bb.x, ((xv[i].y * inv) * gg.y) + bb.y,
                         ((xv[i].z * inv) * gg.z) + bb.z, ((xv[i].w * inv) * gg.w) + bb.w};
     uint32_t packed = 0;
-    bool exact = !FQ;
-    if constexpr (FQ) {
-      uint32_t worst = 0u;  // the largest measure's bit pattern (a NaN measure orders above every finite)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float tf = y[k] * rsf;
-        const float rr = __builtin_rintf(tf);
-        worst = __builtin_elementwise_max(
-            worst, __float_as_uint(__builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, __builtin_fabsf(tf - rr))));
-        // v + 128 of the clamped integer v, in [0, 255]: its byte, flipped to two's complement below
-        packed = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(rr + zp128, lo128, hi128), k, packed);
-      }
-      packed ^= 0x80808080u;
-      exact = __any(worst >= __float_as_uint(0x1.fffffcp-2f));  // (also catches NaN / inf)
-    }
-    if (exact) {
-      packed = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float t = (float)((double)y[k] * rs);
-        const double uu = zp + (double)t;
-        const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
-        packed |= ((uint32_t)(q & 0xff)) << (8 * k);
-      }
+    for (int k = 0; k < 4; ++k) {
+      const float t = (float)((double)y[k] * rs);
+      const double uu = zp + (double)t;
+      const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
+      packed |= ((uint32_t)(q & 0xff)) << (8 * k);
     }
     *reinterpret_cast<uint32_t*>(wl + r * RSO + c0 + 8 * i) = packed;
   }
@@ -2075,19 +2055,13 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
       // 128 / nleaf rows per workgroup (4 waves of 64 / (2 nleaf) rows)
       const int64_t rpw = 128 / p.nleaf;
       const unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
-      // the f32 rounding filter (FQ) for |zp| <= 2^20 (NQK_LN_EXACTQ=1: the f64 chain for every element)
-      const bool fq = zp >= -(1 << 20) && zp <= (1 << 20) && !getenv("NQK_LN_EXACTQ");
-      const float rsf = (float)rs, zp128 = (float)zp + 128.0f, lo128 = (float)lo + 128.0f, hi128 = (float)hi + 128.0f;
-#define LNL(NLV, FQV)                                                                                              \
-  hipLaunchKernelGGL((k_ln_quant_lds<NLV, FQV>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma, beta, out, \
-                     rows, eps, scale, rs, (double)zp, lo, hi, rsf, zp128, lo128, hi128)
-      switch (p.nleaf * 2 + (fq ? 1 : 0)) {
-        case 17: LNL(8, true); break;
-        case 16: LNL(8, false); break;
-        case 9: LNL(4, true); break;
-        case 8: LNL(4, false); break;
-        case 5: LNL(2, true); break;
-        default: LNL(2, false); break;
+#define LNL(NLV)                                                                                                   \
+  hipLaunchKernelGGL((k_ln_quant_lds<NLV>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma, beta, out, \
+                     rows, eps, scale, rs, (double)zp, lo, hi)
+      switch (p.nleaf) {
+        case 8: LNL(8); break;
+        case 4: LNL(4); break;
+        default: LNL(2); break;
       }
 #undef LNL
       return launch_status("nqk_ln_quant(lds)");

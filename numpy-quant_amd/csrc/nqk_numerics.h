@@ -110,6 +110,37 @@ __device__ __forceinline__ v2f_t np_expf_nonpos2(v2f_t x) {
   return v2f_t{__builtin_ldexpf(res[0], (int)q[0]), __builtin_ldexpf(res[1], (int)q[1])};
 }
 
+// np_expf_nonpos2 for x in [NP_EXP_SAFE_LO, 0] (the softmax rows whose smallest argument
+// is there: a wave-uniform test in the attention kernel): q = RN(RN(x log2 e) + 1.5 2^23) -
+// 1.5 2^23 is NumPy's own magic-number rounding (the same integer as v_rndne here), q >= -125
+// keeps poly 2^q normal, so the scaling is an integer add of q << 23 to poly's bits — and
+// q << 23 is the rounded sum's bit pattern shifted left by 23 (1.5 2^23's low 9 bits are
+// zero).  No clamp, no v_cvt / v_ldexp.  Equal to np_expf on every float of the domain
+// (nqk_selftest_fastmath, counts[4]).
+constexpr float NP_EXP_SAFE_LO = -86.5f;
+__device__ __forceinline__ v2f_t np_expf_safe2(v2f_t x) {
+  const float l2e = 1.442695040888963407359924681001892137f;
+  const v2f_t mg = v2f_t{0x1.8p23f, 0x1.8p23f};
+  const v2f_t s = x * v2f_t{l2e, l2e} + mg;
+  const v2f_t q = s - mg;
+  v2f_t r = __builtin_elementwise_fma(q, v2f_t{-6.93145752e-1f, -6.93145752e-1f}, x);
+  r = __builtin_elementwise_fma(q, v2f_t{-1.42860677e-6f, -1.42860677e-6f}, r);
+  auto c2 = [](float c) { return v2f_t{c, c}; };
+  v2f_t num = __builtin_elementwise_fma(c2(5.082762527590693718096e-04f), r, c2(6.757896990527504603057e-03f));
+  num = __builtin_elementwise_fma(num, r, c2(5.114512081637298353406e-02f));
+  num = __builtin_elementwise_fma(num, r, c2(2.473615434895520810817e-01f));
+  num = __builtin_elementwise_fma(num, r, c2(7.257664613233124478488e-01f));
+  num = __builtin_elementwise_fma(num, r, c2(9.999999999980870924916e-01f));
+  v2f_t den = __builtin_elementwise_fma(c2(2.159509375685829852307e-02f), r, c2(-2.742335390411667452936e-01f));
+  den = __builtin_elementwise_fma(den, r, c2(1.0f));
+  const v2f_t rc = v2f_t{__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+  const v2f_t qq = num * rc;
+  const v2f_t e = __builtin_elementwise_fma(-den, qq, num);
+  const v2f_t res = __builtin_elementwise_fma(e, rc, qq);
+  return v2f_t{__uint_as_float(__float_as_uint(res[0]) + (__float_as_uint(s[0]) << 23)),
+               __uint_as_float(__float_as_uint(res[1]) + (__float_as_uint(s[1]) << 23))};
+}
+
 // Round-and-pack of an element pair on the fast path.  c = clamp(x, lo - zp, hi - zp) (med3;
 // clamping before rounding is the same as after for integer bounds), s = RN(c + MAGIC) with
 // MAGIC = 1.5 2^23 + zp: s lies in [2^23, 2^24) where the f32 spacing is 1, so s = rint(c) +

@@ -1543,32 +1543,10 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
         return false;
     }
   };
-  // Tail split: the static schedule runs ceil(nt / slots) rounds; when the last round is at
-  // most half full (N = 768 at B = 256: 1182 tiles = 2.31 rounds on 512 slots) the rows of
-  // the whole rounds go to one launch and the remaining row panels to a second one with one
-  // workgroup per tile, fewer than there are CUs, so each runs alone on its CU (both MFMA
-  // pipes' shares of its SIMDs, no second workgroup's barriers).  Not for QKV (its head
-  // layout addresses rows by image).  NQK_PG_SPLIT=0 disables it.
-  const int rounds = nt / slots, rem = nt - rounds * slots;
-  const char* sv = getenv("NQK_PG_SPLIT");
-  const bool split = !(sv && atoi(sv) == 0) && epi != PG_QKV && rounds >= 1 && rem > 0 && rem <= slots / 2 &&
-                     (int64_t)(rounds * slots / tiles_n) * PG_BM <= M - PG_BM;
-  if (split) {
-    const int p1 = rounds * slots / tiles_n;  // whole row panels of the main launch
-    const int64_t m1 = (int64_t)p1 * PG_BM, m2 = M - m1;
-    const int nt1 = p1 * tiles_n, nt2 = (int)((m2 + PG_BM - 1) / PG_BM) * tiles_n;
-    PgEpi e2 = e;
-    const size_t osz = epi == PG_RESID ? 4 : 1;
-    e2.out[0] = (char*)e.out[0] + (size_t)m1 * N * osz;
-    e2.out[1] = e2.out[2] = e2.out[0];
-    if (epi == PG_RESID) e2.resid = e.resid + (size_t)m1 * N;
-    if (!launch(a, (int)m1, nt1, nt1 < slots ? nt1 : slots, e)) return 0;
-    const int rc1 = launch_status("nqk_qgemm_fused(pg)");
-    if (rc1 < 0) return rc1;
-    if (!launch(a + m1 * lda, (int)m2, nt2, nt2 < slots ? nt2 : slots, e2)) return 0;
-  } else {
-    if (!launch(a, (int)M, nt, nt < slots ? nt : slots, e)) return 0;
-  }
+  // (A tail split — the rows of the whole rounds in one launch, the last round's row panels
+  // in a second launch with one workgroup per tile — measured slower: FFN-down 142 -> 176 us,
+  // out-proj 77 -> 90 us, profiles/r04_pg_split_dropped.txt)
+  if (!launch(a, (int)M, nt, nt < slots ? nt : slots, e)) return 0;
   const int rc = launch_status("nqk_qgemm_fused(pg)");
   return rc < 0 ? rc : (glut ? 6 : 4);
 }

@@ -20,10 +20,28 @@ broadcast / gather through it, so the device path runs on a 1-GPU box
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
+import sys
 
 import numpy as np
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """RCCL prints its version banner on stdout at communicator setup; the bench contract
+    keeps stdout to one JSON line, so file descriptor 1 points at stderr meanwhile (C stdio
+    flushed before it is restored)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def check_gather_sizes(rank: int, world: int, src_bytes: int, dst_bytes) -> None:
@@ -84,10 +102,12 @@ class ReplicaGroup:
         from . import _lib
         uid = (ctypes.c_char * 128)()
         if self.rank == 0:
-            _lib.call("nqk_comm_unique_id", uid)
+            with _stdout_to_stderr():
+                _lib.call("nqk_comm_unique_id", uid)
         raw = self.broadcast_object(bytes(uid))
         uid = (ctypes.c_char * 128).from_buffer_copy(raw)
-        _lib.call("nqk_comm_init", uid, self.world, self.rank)
+        with _stdout_to_stderr():
+            _lib.call("nqk_comm_init", uid, self.world, self.rank)
         self.device_comm = True
 
     def broadcast_qmodel(self, model, qmodel=None):

@@ -35,14 +35,15 @@ def test_fast_division_exp_erf_exhaustive():
     on every one of the 2^32 float inputs, which this test establishes on the device."""
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray
-    counts = DeviceArray.from_host(np.zeros(4, np.uint64))
-    ex = DeviceArray.from_host(np.zeros(4, np.uint32))
+    counts = DeviceArray.from_host(np.zeros(5, np.uint64))
+    ex = DeviceArray.from_host(np.zeros(5, np.uint32))
     _lib.call("nqk_selftest_fastmath", counts.vp, ex.vp)
     c, e = counts.to_host(), ex.to_host()
     assert c[0] == 0, f"fast exp differs on {c[0]} inputs, e.g. {e[0:1].view(np.float32)}"
     assert c[1] == 0, f"fast erf differs on {c[1]} inputs, e.g. {e[1:2].view(np.float32)}"
     assert c[2] == 0, f"non-positive exp differs on {c[2]} inputs, e.g. {e[2:3].view(np.float32)}"
     assert c[3] == 0, f"packed non-positive exp differs on {c[3]} inputs, e.g. {e[3:4].view(np.float32)}"
+    assert c[4] == 0, f"exp on [-86.5, 0] by exponent add differs on {c[4]} inputs, e.g. {e[4:5].view(np.float32)}"
 
 
 def test_gelu_filter_bound_exhaustive():

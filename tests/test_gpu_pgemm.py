@@ -103,8 +103,7 @@ def _numpy_ref(epi_name, M, N, K, host):
     ("resid", 128 * 200, 768, 768, 1.0, False), ("resid", 128 * 200, 768, 3072, 1.0, False),
     ("resid", 128 * 197, 768, 3072, 1.0, True), ("resid", 300, 768, 768, 1.0, False),
     ("resid", 256 * 197, 768, 3072, 1.0, False),
-    # the tail split of pg_launch (a second launch for the row panels of a last round at most
-    # half full), with ragged last rows
+    # ragged last tile rows with more tiles than workgroup slots
     ("gelu", 128 * 50 + 77, 3072, 768, 1.0, False), ("resid", 128 * 200 + 50, 768, 768, 1.0, False),
 ])
 @pytest.mark.parametrize("kernel", [1, 2])

@@ -1,5 +1,6 @@
 #!/usr/bin/env python
-"""Timing of nqk_ln_quant at the ViT-Base B=256 shape (50432 x 768), stream events;
+"""Timing of nqk_ln_quant at the ViT-Base B=256 shape (50432 x 768), stream events, with
+environment variants of the main build interleaved in one process (LNM_ENV="name:VAR=val;...");
 GM_LIB selects a diagnostic build (tools/gemm_diag.sh)."""
 import ctypes
 import os
@@ -33,13 +34,37 @@ def run():
     _lib.call("nqk_ln_quant", x.vp, g.vp, b.vp, out.vp, rows, cols, 1e-12, 0.03, -3, 8)
 
 
-run()
-a, c = ev(), ev()
-_lib.call("nqk_event_record", a)
-for _ in range(20):
-    run()
-_lib.call("nqk_event_record", c)
-ms = ctypes.c_float()
-_lib.call("nqk_event_elapsed", a, c, ctypes.byref(ms))
-us = ms.value / 20 * 1e3
-print(f"ln_quant {rows}x{cols}: {us:.1f} us  {rows * cols * 5 / us / 1e3:.0f} GB/s", flush=True)
+def timed(env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        run()
+        a, c = ev(), ev()
+        _lib.call("nqk_event_record", a)
+        for _ in range(20):
+            run()
+        _lib.call("nqk_event_record", c)
+        ms = ctypes.c_float()
+        _lib.call("nqk_event_elapsed", a, c, ctypes.byref(ms))
+        return ms.value / 20 * 1e3
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+# variants of the main build by environment, interleaved (LNM_ENV="name:VAR=val,...;...")
+variants = {"main": {}}
+for item in filter(None, os.environ.get("LNM_ENV", "").split(";")):
+    name, kv = item.split(":", 1)
+    variants[name] = dict(x.split("=", 1) for x in kv.split(","))
+res = {n: [] for n in variants}
+for _ in range(int(os.environ.get("LNM_ROUNDS", 5))):
+    for n, env in variants.items():
+        res[n].append(timed(env))
+for n, ts in res.items():
+    us = min(ts)
+    print(f"ln_quant[{n}] {rows}x{cols}: min {us:.1f} us  med {sorted(ts)[len(ts) // 2]:.1f} us  "
+          f"{rows * cols * 5 / us / 1e3:.0f} GB/s", flush=True)
