@@ -556,166 +556,6 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
     }
 }
 
-// k_embed_q with a 3-stage LDS ring (round 4): at step kt the waves run k-tile kt's MFMAs
-// on fragments read during step kt - 1, read k-tile kt + 1's fragments (stage (kt + 1) % 3,
-// written before the previous barrier) into the other register set, and write k-tile kt + 2
-// (global loads issued at the step's start) into stage (kt + 2) % 3, last read in step
-// kt - 2.  One barrier per k-tile as before, but no LDS read latency in front of the MFMAs.
-// Same operand images, same k-ordered fmaf chains per BLAS K block: bit-identical to
-// k_embed_q.  60 KiB of LDS (WN = 2), two workgroups per CU.
-template <int WN>
-__global__ void __launch_bounds__(256, 2)
-k_embed_q3(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __restrict__ C, int64_t M, int64_t N,
-           int64_t hw, int64_t wo, int64_t H, int64_t W, float s, float zpf, KBlocks kb, EmbedEpi ee) {
-  typedef float v16f __attribute__((ext_vector_type(16)));
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  constexpr int BN = 64 * WN, K = 768, NKT = K / 16;
-  __shared__ __attribute__((aligned(16))) float sa[3][128 * EQ_ROW];
-  __shared__ __attribute__((aligned(16))) float sb[3][BN * EQ_ROW];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, r32 = lane & 31, h = lane >> 5;
-  const int64_t m0 = (int64_t)blockIdx.y * 128, n0 = (int64_t)blockIdx.x * BN;
-  const int ar = tid & 127, hf = tid >> 7;
-  const int64_t am = m0 + ar < M ? m0 + ar : M - 1;
-  const int64_t img = am / hw, pt = am - img * hw, oy = pt / wo, ox = pt - oy * wo;
-  const int8_t* qrow = q + ((img * 3) * H + oy * 16) * W + ox * 16;
-  const int64_t cstride = H * W;
-  int4 px[3], pxn[3];
-  auto load_px = [&](int ki, int4 (&d)[3]) {
-#pragma unroll
-    for (int ci = 0; ci < 3; ++ci) d[ci] = *reinterpret_cast<const int4*>(qrow + ci * cstride + (int64_t)ki * W);
-  };
-  const int cb = tid >> 2, kq = tid & 3;
-  v4f bv[WN];
-  auto load_b = [&](int kt) {
-#pragma unroll
-    for (int u = 0; u < WN; ++u) {
-      const int64_t n = n0 + cb + 64 * u;
-      bv[u] = n < N ? *reinterpret_cast<const v4f*>(wt + n * K + kt * 16 + 4 * kq) : v4f{0, 0, 0, 0};
-    }
-  };
-  auto store_b = [&](int st) {
-#pragma unroll
-    for (int u = 0; u < WN; ++u) *reinterpret_cast<v4f*>(&sb[st][(cb + 64 * u) * EQ_ROW + 4 * kq]) = bv[u];
-  };
-  auto store_a = [&](int st, auto SUB, const int4 (&d)[3]) __attribute__((always_inline)) {
-    constexpr int sub = decltype(SUB)::value;
-    float f[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int j0 = 16 * sub + e, j1 = 16 * sub + 8 + e;
-      const int kj0 = j0 / 3, c0 = j0 % 3, kj1 = j1 / 3, c1 = j1 % 3;
-      const int w0 = (kj0 >> 2) == 0 ? d[c0].x : (kj0 >> 2) == 1 ? d[c0].y : (kj0 >> 2) == 2 ? d[c0].z : d[c0].w;
-      const int w1 = (kj1 >> 2) == 0 ? d[c1].x : (kj1 >> 2) == 1 ? d[c1].y : (kj1 >> 2) == 2 ? d[c1].z : d[c1].w;
-      const int qv = hf ? (int)(int8_t)(w1 >> (8 * (kj1 & 3))) : (int)(int8_t)(w0 >> (8 * (kj0 & 3)));
-      f[e] = ((float)qv - zpf) * s;
-    }
-    float* dst = &sa[st][ar * EQ_ROW + 4 * hf];
-    *reinterpret_cast<v4f*>(dst) = v4f{f[0], f[2], f[4], f[6]};
-    *reinterpret_cast<v4f*>(dst + 8) = v4f{f[1], f[3], f[5], f[7]};
-  };
-  // fragments of one k-tile: A sub-tiles i, B sub-tiles j, 8 k values each (two b128)
-  v4f fa[2][2][2], fb[2][WN][2];  // [register set][sub-tile][half]
-  auto read_frags = [&](int st, auto SET) __attribute__((always_inline)) {
-    constexpr int r = decltype(SET)::value;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float* src = &sa[st][(wm * 64 + i * 32 + r32) * EQ_ROW + 8 * h];
-      fa[r][i][0] = *reinterpret_cast<const v4f*>(src);
-      fa[r][i][1] = *reinterpret_cast<const v4f*>(src + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const float* src = &sb[st][(wn * 32 * WN + j * 32 + r32) * EQ_ROW + 8 * h];
-      fb[r][j][0] = *reinterpret_cast<const v4f*>(src);
-      fb[r][j][1] = *reinterpret_cast<const v4f*>(src + 4);
-    }
-  };
-  v16f acc[2][WN], tot[2][WN];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = tot[i][j][r] = 0.0f;
-  int blk = 0;
-  int64_t bend = kb.n > 0 ? kb.end[0] : -1;
-  // prologue: k-tiles 0 and 1 (kernel row 0) into stages 0 and 1, fragments of k-tile 0
-  load_px(0, px);
-  load_b(0);
-  store_a(0, std::integral_constant<int, 0>{}, px);
-  store_b(0);
-  load_b(1);
-  store_a(1, std::integral_constant<int, 1>{}, px);
-  store_b(1);
-  __syncthreads();
-  read_frags(0, std::integral_constant<int, 0>{});
-  // step kt: SUB = kt % 3 (kernel-row position), PAR = kt % 2 (fragment register set)
-  auto step = [&](int kt, auto SUB, auto PAR) __attribute__((always_inline)) {
-    constexpr int sub = decltype(SUB)::value, par = decltype(PAR)::value;
-    constexpr int sub2 = (sub + 2) % 3;  // k-tile kt + 2's position in its kernel row
-    const bool more2 = kt + 2 < NKT, more1 = kt + 1 < NKT;
-    if (more2) {
-      load_b(kt + 2);
-      if constexpr (sub2 == 0) load_px((kt + 2) / 3, pxn);
-    }
-    if (more1) read_frags((kt + 1) % 3, std::integral_constant<int, par ^ 1>{});
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < WN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[par][i][kk >> 2][kk & 3], fb[par][j][kk >> 2][kk & 3],
-                                                            acc[i][j], 0, 0, 0);
-    if ((int64_t)kt * 16 + 16 == bend) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < WN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            tot[i][j][r] = tot[i][j][r] + acc[i][j][r];
-            acc[i][j][r] = 0.0f;
-          }
-      ++blk;
-      bend = blk < kb.n ? kb.end[blk] : -1;
-    }
-    if (more2) {
-      if constexpr (sub2 == 0) {
-#pragma unroll
-        for (int ci = 0; ci < 3; ++ci) px[ci] = pxn[ci];
-      }
-      store_a((kt + 2) % 3, std::integral_constant<int, sub2>{}, px);
-      store_b((kt + 2) % 3);
-    }
-    __syncthreads();
-  };
-  for (int k6 = 0; k6 < NKT; k6 += 6) {
-    step(k6, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-    step(k6 + 1, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
-    step(k6 + 2, std::integral_constant<int, 2>{}, std::integral_constant<int, 0>{});
-    step(k6 + 3, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-    step(k6 + 4, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
-    step(k6 + 5, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int64_t gn = n0 + wn * 32 * WN + j * 32 + r32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (gm < M && gn < N) {
-          const uint32_t im = (uint32_t)gm / (uint32_t)ee.hw, t = (uint32_t)gm - im * (uint32_t)ee.hw;
-          const float y = tot[i][j][r] + ee.bias[gn];
-          C[((int64_t)im * (ee.hw + 1) + 1 + t) * N + gn] = y + ee.pos[(1 + (int64_t)t) * N + gn];
-        }
-      }
-    }
-}
-
 // class-token rows of the EMBED output: out[image][0][n] = cls[n] + pos[0][n]
 __global__ void k_embed_cls(const float* __restrict__ cls, const float* __restrict__ pos, float* __restrict__ out,
                             int64_t images, int64_t hw, int64_t n) {
@@ -1061,12 +901,9 @@ extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float
   KBlocks kb;
   if (blas_kblocks(K, &kb) || !kblocks_al16(K, kb)) return fail("nqk_embed_q: K blocking");
   const float zpf = (float)zp;
-  const char* ev = getenv("NQK_EMBED_RING");
-  const bool ring = !(ev && atoi(ev) == 0);
-  if (N % 128 == 0 && ring) {
-    hipLaunchKernelGGL(k_embed_q3<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
-                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw});
-  } else if (N % 128 == 0) {
+  // (a 3-stage LDS ring with the next k-tile's fragments read under the MFMAs measured 1.5 %
+  // slower: 634 vs 625 us, profiles/r04_embed_ring_dropped.txt)
+  if (N % 128 == 0) {
     hipLaunchKernelGGL(k_embed_q<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
                        wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw});
   } else {
