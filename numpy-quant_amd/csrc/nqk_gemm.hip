@@ -450,19 +450,21 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
   };
   // A values of k-tile sub (0..2 within kernel row): k_local = 8 hf + e -> j = 16 sub + k_local,
   // kj = j / 3, ci = j % 3; written at p = (k_local & 1) * 8 + (k_local >> 1)
-  auto store_a = [&](int buf, auto SUB, const int4 (&d)[3]) __attribute__((always_inline)) {
-    constexpr int sub = decltype(SUB)::value;
-    float f[8];
+  // (hf is wave-uniform: a scalar branch picks the half, so each value is one SDWA byte
+  // convert, a subtract and a multiply)
+  auto conv_a = [&](auto SUB, auto HF, const int4 (&d)[3], float (&f)[8]) __attribute__((always_inline)) {
+    constexpr int sub = decltype(SUB)::value, half = decltype(HF)::value;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      // both halves at compile-time offsets, the wave-uniform hf selects
-      const int j0 = 16 * sub + e, j1 = 16 * sub + 8 + e;
-      const int kj0 = j0 / 3, c0 = j0 % 3, kj1 = j1 / 3, c1 = j1 % 3;
-      const int w0 = (kj0 >> 2) == 0 ? d[c0].x : (kj0 >> 2) == 1 ? d[c0].y : (kj0 >> 2) == 2 ? d[c0].z : d[c0].w;
-      const int w1 = (kj1 >> 2) == 0 ? d[c1].x : (kj1 >> 2) == 1 ? d[c1].y : (kj1 >> 2) == 2 ? d[c1].z : d[c1].w;
-      const int qv = hf ? (int)(int8_t)(w1 >> (8 * (kj1 & 3))) : (int)(int8_t)(w0 >> (8 * (kj0 & 3)));
-      f[e] = ((float)qv - zpf) * s;
+      const int j = 16 * sub + 8 * half + e, kj = j / 3, c = j % 3;
+      const int w = (kj >> 2) == 0 ? d[c].x : (kj >> 2) == 1 ? d[c].y : (kj >> 2) == 2 ? d[c].z : d[c].w;
+      f[e] = ((float)(int)(int8_t)(w >> (8 * (kj & 3))) - zpf) * s;
     }
+  };
+  auto store_a = [&](int buf, auto SUB, const int4 (&d)[3]) __attribute__((always_inline)) {
+    float f[8];
+    if (hf) conv_a(SUB, std::integral_constant<int, 1>{}, d, f);
+    else conv_a(SUB, std::integral_constant<int, 0>{}, d, f);
     float* dst = &sa[buf][ar * EQ_ROW + 4 * hf];
     *reinterpret_cast<v4f*>(dst) = v4f{f[0], f[2], f[4], f[6]};      // k_local even -> p = k_local / 2
     *reinterpret_cast<v4f*>(dst + 8) = v4f{f[1], f[3], f[5], f[7]};  // odd -> 8 + k_local / 2
@@ -539,20 +541,32 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
     step(3 * ki + 1, std::integral_constant<int, 1>{});
     step(3 * ki + 2, std::integral_constant<int, 2>{});
   }
+  // epilogue: per output row gm its image im = gm / hw (a float reciprocal, corrected by one
+  // either way: gm < 2^24), output row gm + im + 1 (after the image's class-token row),
+  // position row gm - im hw + 1; bias once per column
+  // (32-bit element offsets: (M + images) N < 2^31, host-checked)
+  const int hwi = (int)ee.hw, Ni = (int)N, Mi = (int)M;
+  const float rhw = 1.0f / (float)hwi;
+  float bj[WN];
+  int gnj[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    gnj[j] = (int)n0 + wn * 32 * WN + j * 32 + r32;
+    bj[j] = gnj[j] < Ni ? ee.bias[gnj[j]] : 0.0f;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int64_t gn = n0 + wn * 32 * WN + j * 32 + r32;
+    for (int r = 0; r < 16; ++r) {
+      const int gm = (int)m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (gm >= Mi) continue;
+      int im = (int)((float)gm * rhw);
+      im = im * hwi > gm ? im - 1 : im;
+      im = (im + 1) * hwi <= gm ? im + 1 : im;
+      const int co = (gm + im + 1) * Ni, po = (gm - im * hwi + 1) * Ni;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (gm < M && gn < N) {
-          const uint32_t im = (uint32_t)gm / (uint32_t)ee.hw, t = (uint32_t)gm - im * (uint32_t)ee.hw;
-          const float y = tot[i][j][r] + ee.bias[gn];
-          C[((int64_t)im * (ee.hw + 1) + 1 + t) * N + gn] = y + ee.pos[(1 + (int64_t)t) * N + gn];
-        }
-      }
+      for (int j = 0; j < WN; ++j)
+        if (gnj[j] < Ni) C[co + gnj[j]] = (tot[i][j][r] + bj[j]) + ee.pos[po + gnj[j]];
     }
 }
 
@@ -898,6 +912,7 @@ extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float
   if ((((uintptr_t)q) | ((uintptr_t)wt)) & 15) return fail("nqk_embed_q: unaligned operands");
   const int64_t wo = w / 16, hw = (h / 16) * wo, M = images * hw, K = 768;
   if ((M + 127) / 128 > 65535) return fail("nqk_embed_q: grid too large");
+  if ((double)(M + images) * (double)N >= 2147483647.0) return fail("nqk_embed_q: output too large");
   KBlocks kb;
   if (blas_kblocks(K, &kb) || !kblocks_al16(K, kb)) return fail("nqk_embed_q: K blocking");
   const float zpf = (float)zp;

@@ -351,7 +351,10 @@ constexpr float PG_QLIM = 0x1.fffffcp-2f;
 // 16 w (the nibble in the high half, its sign bit on the byte's; as nqk_fused.hip
 // k_qgemm_big), so the MFMAs accumulate 16 acc exactly (initial accumulators 16 x the column
 // terms, host-checked to fit int32) and the epilogue takes acc >> 4.
-template <int EPI, int NK, bool F32X, bool B4>
+// S8 (QKV with 8-bit outputs): v_cvt_pk_u8_f32 saturates to [0, 255] (tools/micro/cvtu8.hip:
+// every integral f32 in [-2^24, 2^24], profiles/r04_cvtu8.txt), which is then the clamp, so the
+// v_med3 before it goes.
+template <int EPI, int NK, bool F32X, bool B4, bool S8 = false>
 __global__ void __launch_bounds__(256, 2)
 k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
      PgEpi e) {
@@ -651,9 +654,10 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
             m0 = __builtin_fmaf(__builtin_fabsf(vf[0]), k1, __builtin_fabsf(dd[0]));
             m1 = __builtin_fmaf(__builtin_fabsf(vf[1]), k1, __builtin_fabsf(dd[1]));
             const v2f b = rr + v2f{zp128, zp128};
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[0], e.blo, e.bhi), q & 3, pk[q >> 2]);
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[1], e.blo, e.bhi), (q & 3) + 1,
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(S8 ? b[0] : __builtin_amdgcn_fmed3f(b[0], e.blo, e.bhi), q & 3,
                                                         pk[q >> 2]);
+            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(S8 ? b[1] : __builtin_amdgcn_fmed3f(b[1], e.blo, e.bhi),
+                                                        (q & 3) + 1, pk[q >> 2]);
           } else {  // GELU: h exactly as the reference (F32X), then the filtered fast chain
             const v2f h = v2f{bias[q], bias[q + 1]} + vf * v2f{sacc, sacc};
             hv[q] = h[0];
@@ -1516,7 +1520,8 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   const int slots = 2 * pg_num_cus();
   const int kc = K == 3072 ? 2 : (K == 192 ? 1 : 0);
   const int epi_k = glut ? PG_GLUT : epi;
-  const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0);
+  const bool s8 = epi == PG_QKV && p->bit_width == 8 && !b4 && !getenv("NQK_PG_NOS8");
+  const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0) + (s8 ? 256 : 0);
   auto launch = [&](const int8_t* a_, int m_, int ntiles_, int grid_, const PgEpi& e_) {
     switch (key) {
 #define PGL(E, NKV, X, B)                                                                                      \
@@ -1524,6 +1529,14 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     hipLaunchKernelGGL((k_pg<E, NKV, X, B>), dim3(grid_), dim3(256), pg_lds_bytes(E, B), stream(), a_, bp, m_,  \
                        (int)N, (int)lda, tiles_n, ntiles_, e_);                                                \
     return true;
+      case 256 + PG_QKV * 16 + 0 * 4 + 1:  // QKV, 8-bit outputs: the saturating convert clamps
+        hipLaunchKernelGGL((k_pg<PG_QKV, 12, true, false, true>), dim3(grid_), dim3(256), pg_lds_bytes(PG_QKV, false),
+                           stream(), a_, bp, m_, (int)N, (int)lda, tiles_n, ntiles_, e_);
+        return true;
+      case 256 + PG_QKV * 16 + 1 * 4 + 1:
+        hipLaunchKernelGGL((k_pg<PG_QKV, 3, true, false, true>), dim3(grid_), dim3(256), pg_lds_bytes(PG_QKV, false),
+                           stream(), a_, bp, m_, (int)N, (int)lda, tiles_n, ntiles_, e_);
+        return true;
       PGL(PG_QKV, 12, true, false)
       PGL(PG_GELU, 12, true, false)
       PGL(PG_GLUT, 12, true, false)

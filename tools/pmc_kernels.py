@@ -1,7 +1,9 @@
 """Per-kernel PMC table from rocprofv3 --pmc passes: for every kernel name (template
 arguments kept, namespaces stripped) the mean over its dispatches of each counter and of the
 kernel-trace duration, across any number of pass directories.
-Usage: python tools/pmc_kernels.py <pass dir> [<pass dir> ...] [--match SUBSTR] [--json OUT]"""
+Usage: python tools/pmc_kernels.py <pass dir> [<pass dir> ...] [--match SUBSTR] [--json OUT] [--by-grid]
+(--by-grid: one row per kernel name and grid size, e.g. to keep a bench's B = 256 forward apart
+from its small calibration batch)"""
 import csv
 import glob
 import json
@@ -18,12 +20,15 @@ def short(name):
 
 
 def main(argv):
-    dirs, match, out = [], "", None
+    dirs, match, out, by_grid = [], "", None, False
     i = 0
     while i < len(argv):
         if argv[i] == "--match":
             match = argv[i + 1]
             i += 2
+        elif argv[i] == "--by-grid":
+            by_grid = True
+            i += 1
         elif argv[i] == "--json":
             out = argv[i + 1]
             i += 2
@@ -39,6 +44,8 @@ def main(argv):
                 k = short(row["Kernel_Name"])
                 if match not in k:
                     continue
+                if by_grid:
+                    k += f" [grid {row['Grid_Size']}]"
                 per[(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
                 names[row["Dispatch_Id"]] = k
             for (disp, c), v in per.items():
@@ -48,6 +55,8 @@ def main(argv):
                 k = short(row["Kernel_Name"])
                 if match not in k:
                     continue
+                if by_grid:
+                    k += f" [grid {int(row['Grid_Size_X']) * int(row['Grid_Size_Y']) * int(row['Grid_Size_Z'])}]"
                 vals[k]["duration_us"].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
     res = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
     for k in sorted(res):
