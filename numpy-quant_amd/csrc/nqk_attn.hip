@@ -36,11 +36,29 @@
 #ifndef NQK_ATTN_EXP2
 #define NQK_ATTN_EXP2 1  // 1: rows whose arguments all lie in [-86.5, 0] take np_expf_safe2
 #endif
+#ifndef NQK_ATTN_QDMA
+#define NQK_ATTN_QDMA 0  // 1: each wave's Q row tiles go to LDS by LDS-DMA at the start (with the K/V staging)
+#endif
 #ifndef NQK_ATTN_PSUM
 #define NQK_ATTN_PSUM 1  // 1: the pairwise-sum accumulators as packed pairs (v_pk_add_f32)
 #endif
 
 namespace nqk {
+#if (NQK_ATTN_DIAG & 128)
+// diagnostic builds: per launch, wave-tiles that took [0] the clamped exp (some argument below
+// -86.5), [1] the clamped P quantize, [2] the P exact fallback, [3] the context exact fallback
+__device__ unsigned long long g_attn_stats[4];
+extern "C" int nqk_attn_diag_stats(unsigned long long* out, int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_stats), 4 * sizeof(unsigned long long));
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  if (reset) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stats), z, sizeof(z));
+  return 0;
+}
+#define NQK_ATTN_COUNT(i) \
+  do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_attn_stats[i], 1ull); } while (0)
+#else
+#define NQK_ATTN_COUNT(i) do { } while (0)
+#endif
 namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -136,6 +154,24 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   const int8_t* k = Kg + (int64_t)bh * T * 64;
   const int8_t* v = Vg + (int64_t)bh * T * 64;
 
+  // NQK_ATTN_QDMA: the wave's Q row tiles (rt = wave, wave + 4; 2 KiB each, rows past T
+  // clamped to T - 1) by LDS-DMA, issued before the K/V loads; landed by the staging barrier
+  int8_t* const qlds = reinterpret_cast<int8_t*>(colV + 64);
+  if constexpr (NQK_ATTN_QDMA) {
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(q), (short)0, T * 64, 0x00020000);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int rt = wave + 4 * sl;
+      if (rt < NT) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = min(rt * 32 + 16 * j + (lane >> 2), T - 1);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (__attribute__((address_space(3))) void*)(qlds + wave * 4096 + sl * 2048 + 1024 * j),
+                                                   16, (uint32_t)(row * 64 + (lane & 3) * 16), 0u, 0, 0);
+        }
+      }
+    }
+  }
   // ---- K (swizzled) and V^T (zero padded) into LDS, zero-point column terms
   for (int idx = tid; idx < TP * 4; idx += 256) {
     const int row = idx >> 2, ch = idx & 3;
@@ -174,6 +210,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     }
 #endif
   }
+  if constexpr (NQK_ATTN_QDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the Q DMA landed
   __syncthreads();
   for (int row = tid; row < TP; row += 256) {
     const v4i* kr = reinterpret_cast<const v4i*>(Ks + row * 64);
@@ -204,7 +241,11 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   for (int rt = wave; rt < NT; rt += 4) {
     const int m0 = rt * 32, m = m0 + r32;
     v4i qb[2];
-    {
+    if constexpr (NQK_ATTN_QDMA) {  // from the wave's LDS copy (rows past T: row T - 1)
+      const int8_t* qs = qlds + wave * 4096 + (rt >> 2) * 2048 + r32 * 64;
+      qb[0] = *reinterpret_cast<const v4i*>(qs + h * 16);
+      qb[1] = *reinterpret_cast<const v4i*>(qs + (2 + h) * 16);
+    } else {
       const int qrow = min(m, T - 1);
       qb[0] = *reinterpret_cast<const v4i*>(q + qrow * 64 + h * 16);
       qb[1] = *reinterpret_cast<const v4i*>(q + qrow * 64 + (2 + h) * 16);
@@ -286,6 +327,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     // NQK_ATTN_EXP2: every argument y - max of the whole groups in [-86.5, 0] in all lanes
     // (RN(mn - mx) is the smallest; straddling groups keep np_expf_nonpos2 for their -inf pads)
     const bool esafe = NQK_ATTN_EXP2 && __all(mn + nm >= NP_EXP_SAFE_LO);
+    if (!esafe) NQK_ATTN_COUNT(0);
     if (FAST && NQK_ATTN_PK && NQK_ATTN_EXP2 && TC > 0 && (NQK_ATTN_DIAG & 2) == 0) {
 #pragma unroll
       for (int c = 0; c < NT; ++c) {
@@ -427,6 +469,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     // 2^-24 off for it)
     const bool pq_nc = NQK_ATTN_PQ2 && pqlo <= 0.0f && __all(kpf <= pqhi);
     const float plim2 = plim - 0x1p-24f;
+    if (!pq_nc) NQK_ATTN_COUNT(1);
     v16i acc2[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -470,6 +513,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             dw[qq] = (int)w;
           }
           if (__builtin_expect(__any(!(worst < plim2)), 0)) {
+            NQK_ATTN_COUNT(2);
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) {
               if (pad_group(c, qq)) continue;
@@ -526,6 +570,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           dw[qq] = (int)(packed ^ 0x80808080u);
         }
         if (__builtin_expect(__any(!(worst < plim)), 0)) {
+          NQK_ATTN_COUNT(2);
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq) {
             if (pad_group(c, qq)) continue;
@@ -626,6 +671,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
                                                         __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3)));
           packed = pack4_low(s0, s1);
           if (__builtin_expect(__any(wm >= __float_as_uint(0x1.fffffcp-2f)), 0)) {
+            NQK_ATTN_COUNT(3);
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
               const int qv = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
@@ -719,7 +765,8 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   const bool fast = bs < 16777216.0 && bp < 16777216.0 && dm == 0.5f && llabs(p->zp_ctx) < (1 << 20) &&
                     normal(a.s_qkd) && normal(p->s_qk) &&
                     !getenv("NQK_ATTN_EXACT");
-  const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + 256 + (size_t)(NT * 32 + 64) * 4;
+  const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + 256 + (size_t)(NT * 32 + 64) * 4 +
+                    (NQK_ATTN_QDMA ? 4 * 4096 : 0);
   const dim3 grid((unsigned)batch_heads);
   switch (T == 197 ? (fast ? -1 : 0) : NT) {
 #define A(n) case n: hipLaunchKernelGGL((k_attention<n, 0, false>), grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;

@@ -1614,16 +1614,25 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int8_t* const wl = lds + wave * WLDS;
-  const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * RW;
-  if (row0 >= rows) return;  // (uniform per wave; no workgroup barrier follows)
+  // two row groups per wave (round 4): right after the first group's rows are in the LDS
+  // image, the same registers load the second group, whose loads are then in flight during
+  // the first group's tree, quantize and stores (a compile-time loop: the registers stay
+  // registers)
+  constexpr int GPW = 2;
+  const int64_t nrg = (rows + RW - 1) / RW, gstride = (int64_t)gridDim.x * 4;
+  int64_t rg = (int64_t)blockIdx.x * 4 + wave;
+  if (rg >= nrg) return;  // (uniform per wave; no workgroup barrier follows)
   // ---- linear loads (rows past the end read the last row; not stored)
   float4 ld[NLD];
 #pragma unroll
   for (int k = 0; k < NLD; ++k) {
     const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
-    const int64_t gr = row0 + r < rows ? row0 + r : rows - 1;
+    const int64_t gr = rg * RW + r < rows ? rg * RW + r : rows - 1;
     ld[k] = *reinterpret_cast<const float4*>(x + gr * COLS + c * 4);
   }
+#pragma unroll
+  for (int it = 0; it < GPW; ++it) {
+  const int64_t row0 = rg * RW;
 #pragma unroll
   for (int k = 0; k < NLD; ++k) {
     const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
@@ -1631,6 +1640,16 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
+  const bool more = it + 1 < GPW && rg + gstride < nrg;
+  if (it + 1 < GPW) {  // (a wave without a second group reloads its own rows: a conditional
+                       // load would send ld through scratch)
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
+      const int64_t g2 = (more ? rg + gstride : rg) * RW + r;
+      ld[k] = *reinterpret_cast<const float4*>(x + (g2 < rows ? g2 : rows - 1) * COLS + c * 4);
+    }
+  }
   // ---- the tree layout: lane (row r, leaf, grp) holds columns leaf*96 + 8i + 4grp + 0..3
   const int r = lane / LPR, u = lane % LPR, leaf = u >> 1, grp = u & 1;
   const int c0 = leaf * LF + 4 * grp;
@@ -1690,6 +1709,12 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
     const int C = k * 64 + lane, rr = C / (COLS / 16), c = C - rr * (COLS / 16);
     const v4i v = *reinterpret_cast<const v4i*>(wl + rr * RSO + c * 16);
     if (row0 + rr < rows) *reinterpret_cast<v4i*>(out + (row0 + rr) * COLS + c * 16) = v;
+  }
+  if (!more) break;
+  // the stores' image reads are done before the next group overwrites the image
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  rg += gstride;
   }
 }
 constexpr int ln_lds_bytes(int nl) { return 4 * (64 / (2 * nl)) * (nl * 96 * 4 + nl * 16); }
@@ -2054,7 +2079,10 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
     if (!getenv("NQK_LN_REG")) {  // rows through LDS: linear 1 KiB loads / stores per wave
       // 128 / nleaf rows per workgroup (4 waves of 64 / (2 nleaf) rows)
       const int64_t rpw = 128 / p.nleaf;
-      const unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
+      unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
+      // two row groups per wave (the second group's loads under the first's work);
+      // NQK_LN_GPW1=1: one group per wave
+      if (!getenv("NQK_LN_GPW1")) gl = (gl + 1) / 2;
 #define LNL(NLV)                                                                                                   \
   hipLaunchKernelGGL((k_ln_quant_lds<NLV>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma, beta, out, \
                      rows, eps, scale, rs, (double)zp, lo, hi)
