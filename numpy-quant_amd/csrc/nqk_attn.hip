@@ -252,12 +252,18 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     }
     int rq = sum16a(qb[0]) + sum16a(qb[1]);
     rq += xor32i(rq);
-    const int rowterm = rq * a.zk;
+    // minus the row term: acc init = nrowterm - colterm, one v_sub per element (the empty asm
+    // keeps the compiler from re-associating it into -(rowterm + colterm): an add and a sub)
+    int nrowterm = -(rq * a.zk);
+    asm volatile("" : "+v"(nrowterm));
     // ---- per score tile c: S^T = K Q^T (two MFMAs), dequant + Div (EPI_SCORES), row
     // max; only one tile's accumulators are live
     float e[NT][16];
     float mx = -__builtin_inff();
     float mn = __builtin_inff();  // NQK_ATTN_EXP2: the smallest score of the whole groups
+    // whole groups: max / min of the integers (y = RN(v s_qkd) is monotone in v for s_qkd > 0,
+    // host-checked on the FAST path), one v_max3_i32 / v_min3_i32 per pair; converted once
+    int imx = INT32_MIN, imn = INT32_MAX;
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
       // the accumulators start at -(row term + column term): the MFMAs then leave the
@@ -272,7 +278,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         }
         const v4i ck = *reinterpret_cast<const v4i*>(colK + c * 32 + 8 * qq + 4 * h);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[4 * qq + j] = -(rowterm + ck[j]);
+        for (int j = 0; j < 4; ++j) acc[4 * qq + j] = nrowterm - ck[j];
       }
 #pragma unroll
       for (int s = 0; s < 2 && (NQK_ATTN_DIAG & 8) == 0; ++s) {  // (diagnostic 8: no score MFMAs)
@@ -297,8 +303,12 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             if (!full) y = y + v2f_t{n < T ? 0.0f : -__builtin_inff(), n + 1 < T ? 0.0f : -__builtin_inff()};
             e[c][r] = y[0];
             e[c][r + 1] = y[1];
-            mx = __builtin_fmaxf(mx, __builtin_fmaxf(y[0], y[1]));
-            if (NQK_ATTN_EXP2 && full) mn = __builtin_fminf(mn, __builtin_fminf(y[0], y[1]));
+            if (full) {
+              imx = max(imx, max(acc[r], acc[r + 1]));
+              if (NQK_ATTN_EXP2) imn = min(imn, min(acc[r], acc[r + 1]));
+            } else {
+              mx = __builtin_fmaxf(mx, __builtin_fmaxf(y[0], y[1]));
+            }
           }
           __builtin_amdgcn_sched_barrier(0);
           continue;
@@ -318,6 +328,10 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+    }
+    if constexpr (FAST && NQK_ATTN_PK) {
+      if (imx != INT32_MIN) mx = __builtin_fmaxf(mx, (float)imx * a.s_qkd);
+      if (NQK_ATTN_EXP2 && imn != INT32_MAX) mn = (float)imn * a.s_qkd;
     }
     {
       const float o = xor32f(mx);
@@ -763,7 +777,7 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   int dexp = 0;
   const float dm = frexpf(p->div, &dexp);
   const bool fast = bs < 16777216.0 && bp < 16777216.0 && dm == 0.5f && llabs(p->zp_ctx) < (1 << 20) &&
-                    normal(a.s_qkd) && normal(p->s_qk) &&
+                    normal(a.s_qkd) && normal(p->s_qk) && a.s_qkd > 0.0f &&
                     !getenv("NQK_ATTN_EXACT");
   const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + 256 + (size_t)(NT * 32 + 64) * 4 +
                     (NQK_ATTN_QDMA ? 4 * 4096 : 0);
