@@ -1596,9 +1596,10 @@ k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const f
 // 96-column leaf: conflict-free reads in the tree layout), read in the tree layout,
 // and the packed int8 results written back into LDS (784-B rows: conflict-free dword
 // writes) and stored linearly.  No workgroup barrier: each wave owns its LDS image.
-// (An f32 rounding filter in front of the f64 quantize chain measured slower here: 40.9 vs
-// 39.3 us per launch at 50432 x 768, profiles/r04_ln_filter_dropped.txt — the kernel is bound
-// by its loads and stores, not by the quantize.)
+// (Measured slower and dropped in round 4: an f32 rounding filter in front of the f64
+// quantize chain, 40.9 vs 39.3 us per launch at 50432 x 768, profiles/r04_ln_filter_dropped.txt;
+// two row groups per wave with the second group's loads under the first's work, 40.8 vs
+// 39.7 us, profiles/r04_ln_gpw_dropped.txt.)
 template <int NL>
 __global__ void __launch_bounds__(256)
 k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
@@ -1614,25 +1615,16 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int8_t* const wl = lds + wave * WLDS;
-  // two row groups per wave (round 4): right after the first group's rows are in the LDS
-  // image, the same registers load the second group, whose loads are then in flight during
-  // the first group's tree, quantize and stores (a compile-time loop: the registers stay
-  // registers)
-  constexpr int GPW = 2;
-  const int64_t nrg = (rows + RW - 1) / RW, gstride = (int64_t)gridDim.x * 4;
-  int64_t rg = (int64_t)blockIdx.x * 4 + wave;
-  if (rg >= nrg) return;  // (uniform per wave; no workgroup barrier follows)
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * RW;
+  if (row0 >= rows) return;  // (uniform per wave; no workgroup barrier follows)
   // ---- linear loads (rows past the end read the last row; not stored)
   float4 ld[NLD];
 #pragma unroll
   for (int k = 0; k < NLD; ++k) {
     const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
-    const int64_t gr = rg * RW + r < rows ? rg * RW + r : rows - 1;
+    const int64_t gr = row0 + r < rows ? row0 + r : rows - 1;
     ld[k] = *reinterpret_cast<const float4*>(x + gr * COLS + c * 4);
   }
-#pragma unroll
-  for (int it = 0; it < GPW; ++it) {
-  const int64_t row0 = rg * RW;
 #pragma unroll
   for (int k = 0; k < NLD; ++k) {
     const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
@@ -1640,16 +1632,6 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  const bool more = it + 1 < GPW && rg + gstride < nrg;
-  if (it + 1 < GPW) {  // (a wave without a second group reloads its own rows: a conditional
-                       // load would send ld through scratch)
-#pragma unroll
-    for (int k = 0; k < NLD; ++k) {
-      const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
-      const int64_t g2 = (more ? rg + gstride : rg) * RW + r;
-      ld[k] = *reinterpret_cast<const float4*>(x + (g2 < rows ? g2 : rows - 1) * COLS + c * 4);
-    }
-  }
   // ---- the tree layout: lane (row r, leaf, grp) holds columns leaf*96 + 8i + 4grp + 0..3
   const int r = lane / LPR, u = lane % LPR, leaf = u >> 1, grp = u & 1;
   const int c0 = leaf * LF + 4 * grp;
@@ -1709,12 +1691,6 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
     const int C = k * 64 + lane, rr = C / (COLS / 16), c = C - rr * (COLS / 16);
     const v4i v = *reinterpret_cast<const v4i*>(wl + rr * RSO + c * 16);
     if (row0 + rr < rows) *reinterpret_cast<v4i*>(out + (row0 + rr) * COLS + c * 16) = v;
-  }
-  if (!more) break;
-  // the stores' image reads are done before the next group overwrites the image
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  rg += gstride;
   }
 }
 constexpr int ln_lds_bytes(int nl) { return 4 * (64 / (2 * nl)) * (nl * 96 * 4 + nl * 16); }
@@ -2079,10 +2055,7 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
     if (!getenv("NQK_LN_REG")) {  // rows through LDS: linear 1 KiB loads / stores per wave
       // 128 / nleaf rows per workgroup (4 waves of 64 / (2 nleaf) rows)
       const int64_t rpw = 128 / p.nleaf;
-      unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
-      // two row groups per wave (the second group's loads under the first's work);
-      // NQK_LN_GPW1=1: one group per wave
-      if (!getenv("NQK_LN_GPW1")) gl = (gl + 1) / 2;
+      const unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
 #define LNL(NLV)                                                                                                   \
   hipLaunchKernelGGL((k_ln_quant_lds<NLV>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma, beta, out, \
                      rows, eps, scale, rs, (double)zp, lo, hi)

@@ -28,7 +28,7 @@ model, qmodel = bench.build_vit(B, 8, group)
 x = np.random.default_rng(256).standard_normal((B, 3, 224, 224)).astype(np.float32)
 qmodel([FTensor(x)])
 plan = qmodel._plan
-layer = [s for s in plan.steps if isinstance(s, FusedLayer)][-1]
+layer = [o for _, o in plan.steps if isinstance(o, FusedLayer)][-1]
 w = plan.ws.bufs
 m = layer.m
 H, T, Dh, D = m.heads, m.tokens, m.hdim, layer.D
