@@ -36,8 +36,8 @@
 #ifndef NQK_ATTN_EXP2
 #define NQK_ATTN_EXP2 1  // 1: rows whose arguments all lie in [-86.5, 0] take np_expf_safe2
 #endif
-#ifndef NQK_ATTN_QDMA
-#define NQK_ATTN_QDMA 0  // 1: each wave's Q row tiles go to LDS by LDS-DMA at the start (with the K/V staging)
+#ifndef NQK_ATTN_PREL
+#define NQK_ATTN_PREL 1  // 1: P filter margin per element (|tf| 2^-21) instead of the row's (kpf 2^-20)
 #endif
 #ifndef NQK_ATTN_PSUM
 #define NQK_ATTN_PSUM 1  // 1: the pairwise-sum accumulators as packed pairs (v_pk_add_f32)
@@ -154,24 +154,6 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   const int8_t* k = Kg + (int64_t)bh * T * 64;
   const int8_t* v = Vg + (int64_t)bh * T * 64;
 
-  // NQK_ATTN_QDMA: the wave's Q row tiles (rt = wave, wave + 4; 2 KiB each, rows past T
-  // clamped to T - 1) by LDS-DMA, issued before the K/V loads; landed by the staging barrier
-  int8_t* const qlds = reinterpret_cast<int8_t*>(colV + 64);
-  if constexpr (NQK_ATTN_QDMA) {
-    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(q), (short)0, T * 64, 0x00020000);
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-      const int rt = wave + 4 * sl;
-      if (rt < NT) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int row = min(rt * 32 + 16 * j + (lane >> 2), T - 1);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (__attribute__((address_space(3))) void*)(qlds + wave * 4096 + sl * 2048 + 1024 * j),
-                                                   16, (uint32_t)(row * 64 + (lane & 3) * 16), 0u, 0, 0);
-        }
-      }
-    }
-  }
   // ---- K (swizzled) and V^T (zero padded) into LDS, zero-point column terms
   for (int idx = tid; idx < TP * 4; idx += 256) {
     const int row = idx >> 2, ch = idx & 3;
@@ -210,7 +192,6 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     }
 #endif
   }
-  if constexpr (NQK_ATTN_QDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the Q DMA landed
   __syncthreads();
   for (int row = tid; row < TP; row += 256) {
     const v4i* kr = reinterpret_cast<const v4i*>(Ks + row * 64);
@@ -241,11 +222,9 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   for (int rt = wave; rt < NT; rt += 4) {
     const int m0 = rt * 32, m = m0 + r32;
     v4i qb[2];
-    if constexpr (NQK_ATTN_QDMA) {  // from the wave's LDS copy (rows past T: row T - 1)
-      const int8_t* qs = qlds + wave * 4096 + (rt >> 2) * 2048 + r32 * 64;
-      qb[0] = *reinterpret_cast<const v4i*>(qs + h * 16);
-      qb[1] = *reinterpret_cast<const v4i*>(qs + (2 + h) * 16);
-    } else {
+    {
+      // (Q rows by LDS-DMA at the workgroup's start instead: no faster on the bench's data,
+      // profiles/r04_attn_real_data.txt)
       const int qrow = min(m, T - 1);
       qb[0] = *reinterpret_cast<const v4i*>(q + qrow * 64 + h * 16);
       qb[1] = *reinterpret_cast<const v4i*>(q + qrow * 64 + (2 + h) * 16);
@@ -514,8 +493,18 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             const v2f_t s0 = __builtin_elementwise_fma(e0, k2, m2), s1 = __builtin_elementwise_fma(e1, k2, m2);
             const v2f_t dd0 = __builtin_elementwise_fma(e0, k2, -(s0 - m2));
             const v2f_t dd1 = __builtin_elementwise_fma(e1, k2, -(s1 - m2));
-            worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd0[0]), __builtin_fabsf(dd0[1])));
-            worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd1[0]), __builtin_fabsf(dd1[1])));
+            if constexpr (NQK_ATTN_PREL) {
+              // |t - e kpf| <= 3 2^-24 |t|: the margin 2^-21 |r| (r = the rounded value; at r = 0
+              // the limit itself covers it), the limit 0.5 - 2^-22 absorbs dd's own rounding
+              const v2f_t r0 = s0 - m2, r1 = s1 - m2;
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(r0[0]), 0x1p-21f, __builtin_fabsf(dd0[0])),
+                                                             __builtin_fmaf(__builtin_fabsf(r0[1]), 0x1p-21f, __builtin_fabsf(dd0[1]))));
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(r1[0]), 0x1p-21f, __builtin_fabsf(dd1[0])),
+                                                             __builtin_fmaf(__builtin_fabsf(r1[1]), 0x1p-21f, __builtin_fabsf(dd1[1]))));
+            } else {
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd0[0]), __builtin_fabsf(dd0[1])));
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd1[0]), __builtin_fabsf(dd1[1])));
+            }
             uint32_t w = pack4_low(s0, s1);
             if (!(TC > 0 && c * 32 + 8 * qq + 8 <= TC)) {  // padded columns: 0
               const int n = c * 32 + 8 * qq + 4 * h;
@@ -526,7 +515,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             }
             dw[qq] = (int)w;
           }
-          if (__builtin_expect(__any(!(worst < plim2)), 0)) {
+          if (__builtin_expect(__any(!(worst < (NQK_ATTN_PREL ? 0x1.fffff8p-2f : plim2))), 0)) {
             NQK_ATTN_COUNT(2);
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) {
@@ -535,8 +524,10 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
               for (int j = 0; j < 4; ++j) {
                 const int n = c * 32 + 8 * qq + 4 * h + j;
                 const float x = e[c][4 * qq + j];
-                const float d = __builtin_fmaf(x, kpf, -((__builtin_fmaf(x, kpf, pmagic)) - pmagic));
-                if (!(__builtin_fabsf(d) < plim2)) {
+                const float rr = __builtin_fmaf(x, kpf, pmagic) - pmagic;
+                const float d = __builtin_fmaf(x, kpf, -rr);
+                if (!(NQK_ATTN_PREL ? __builtin_fmaf(__builtin_fabsf(rr), 0x1p-21f, __builtin_fabsf(d)) < 0x1.fffff8p-2f
+                                    : __builtin_fabsf(d) < plim2)) {
                   const int qv = n < T ? quant_w(div_rc_w(x, rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) : 0;
                   dw[qq] = (int)(((uint32_t)dw[qq] & ~(0xffu << (8 * j))) | ((uint32_t)(qv & 0xff) << (8 * j)));
                 }
@@ -554,11 +545,21 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             // pairs: one v_pk_mul for tf, the clamp / magic-number rounding + byte pack of
             // round_magic2 / pack4_low (nqk_numerics.h), |dd| into the tile's worst
             v2f_t dd0, dd1;
-            const v2f_t s0 = round_magic2(v2f_t{e[c][4 * qq], e[c][4 * qq + 1]} * v2f_t{kpf, kpf}, pqlo, pqhi, pmagic, dd0);
-            const v2f_t s1 =
-                round_magic2(v2f_t{e[c][4 * qq + 2], e[c][4 * qq + 3]} * v2f_t{kpf, kpf}, pqlo, pqhi, pmagic, dd1);
-            worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd0[0]), __builtin_fabsf(dd0[1])));
-            worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd1[0]), __builtin_fabsf(dd1[1])));
+            const v2f_t tf0 = v2f_t{e[c][4 * qq], e[c][4 * qq + 1]} * v2f_t{kpf, kpf};
+            const v2f_t tf1 = v2f_t{e[c][4 * qq + 2], e[c][4 * qq + 3]} * v2f_t{kpf, kpf};
+            const v2f_t s0 = round_magic2(tf0, pqlo, pqhi, pmagic, dd0);
+            const v2f_t s1 = round_magic2(tf1, pqlo, pqhi, pmagic, dd1);
+            if constexpr (NQK_ATTN_PREL) {
+              // |t - tf| <= 4 2^-24 |t|: the margin 2^-21 |tf| per element (clamped elements:
+              // dd = 0, and the clamp decides them either way)
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(tf0[0]), 0x1p-21f, __builtin_fabsf(dd0[0])),
+                                                             __builtin_fmaf(__builtin_fabsf(tf0[1]), 0x1p-21f, __builtin_fabsf(dd0[1]))));
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(tf1[0]), 0x1p-21f, __builtin_fabsf(dd1[0])),
+                                                             __builtin_fmaf(__builtin_fabsf(tf1[1]), 0x1p-21f, __builtin_fabsf(dd1[1]))));
+            } else {
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd0[0]), __builtin_fabsf(dd0[1])));
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd1[0]), __builtin_fabsf(dd1[1])));
+            }
             uint32_t w = pack4_low(s0, s1);
             if (!(TC > 0 && c * 32 + 8 * qq + 8 <= TC)) {  // padded columns: 0
               const int n = c * 32 + 8 * qq + 4 * h;
@@ -583,7 +584,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           }
           dw[qq] = (int)(packed ^ 0x80808080u);
         }
-        if (__builtin_expect(__any(!(worst < plim)), 0)) {
+        const bool prel = NQK_ATTN_PREL && NQK_ATTN_PK;
+        if (__builtin_expect(__any(!(worst < (prel ? 0x1.fffff8p-2f : plim))), 0)) {
           NQK_ATTN_COUNT(2);
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq) {
@@ -592,7 +594,9 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             for (int j = 0; j < 4; ++j) {
               const int n = c * 32 + 8 * qq + 4 * h + j;
               const float tf = e[c][4 * qq + j] * kpf;
-              if (!(__builtin_fabsf(tf - __builtin_rintf(tf)) < plim)) {
+              const float cf = prel ? __builtin_amdgcn_fmed3f(tf, pqlo, pqhi) : tf;  // (the clamp as in the fast path)
+              const float dv = __builtin_fabsf(cf - __builtin_rintf(cf));
+              if (!(prel ? __builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, dv) < 0x1.fffff8p-2f : dv < plim)) {
                 const int qv = n < T ? quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) : 0;
                 dw[qq] = (int)(((uint32_t)dw[qq] & ~(0xffu << (8 * j))) | ((uint32_t)(qv & 0xff) << (8 * j)));
               }
@@ -779,8 +783,7 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   const bool fast = bs < 16777216.0 && bp < 16777216.0 && dm == 0.5f && llabs(p->zp_ctx) < (1 << 20) &&
                     normal(a.s_qkd) && normal(p->s_qk) && a.s_qkd > 0.0f &&
                     !getenv("NQK_ATTN_EXACT");
-  const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + 256 + (size_t)(NT * 32 + 64) * 4 +
-                    (NQK_ATTN_QDMA ? 4 * 4096 : 0);
+  const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + 256 + (size_t)(NT * 32 + 64) * 4;
   const dim3 grid((unsigned)batch_heads);
   switch (T == 197 ? (fast ? -1 : 0) : NT) {
 #define A(n) case n: hipLaunchKernelGGL((k_attention<n, 0, false>), grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;

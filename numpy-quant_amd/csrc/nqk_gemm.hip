@@ -570,158 +570,6 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
     }
 }
 
-// k_embed_q with one workgroup per CU (round 4): 256 x 128 tiles, 4 waves of 128 x 64 (4 x 2
-// blocks of 32 x 32), i.e. ONE wave per SIMD.  The f32 MFMA runs on the SIMD's f32 datapath
-// (SQ_VALU_MFMA_COEXEC_CYCLES = 0 for k_embed_q), so two waves per SIMD serialize each other's
-// VALU with their MFMAs; a lone wave issues its own conversion / LDS work between its
-// MFMAs instead (MI355X_MICROARCH.md: an f32 32x32x2 MFMA holds the vector issue for part of
-// its 64 cycles).  Same operand images, same k-ordered fmaf chains per BLAS K block:
-// bit-identical to k_embed_q.  Each thread converts one A row (all 16 k values of a k-tile).
-__global__ void __launch_bounds__(256, 1)
-k_embed_q4(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __restrict__ C, int64_t M, int64_t N,
-           int64_t hw, int64_t wo, int64_t H, int64_t W, float s, float zpf, KBlocks kb, EmbedEpi ee) {
-  typedef float v16f __attribute__((ext_vector_type(16)));
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  constexpr int BM = 256, BN = 128, K = 768, NKT = K / 16;
-  __shared__ __attribute__((aligned(16))) float sa[2][BM * EQ_ROW];
-  __shared__ __attribute__((aligned(16))) float sb[2][BN * EQ_ROW];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, r32 = lane & 31, h = lane >> 5;
-  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
-  // A: thread tid converts row tid of the tile
-  const int64_t am = m0 + tid < M ? m0 + tid : M - 1;
-  const int64_t img = am / hw, pt = am - img * hw, oy = pt / wo, ox = pt - oy * wo;
-  const int8_t* qrow = q + ((img * 3) * H + oy * 16) * W + ox * 16;
-  const int64_t cstride = H * W;
-  int4 px[3], pxn[3];
-  auto load_px = [&](int ki, int4 (&d)[3]) {
-#pragma unroll
-    for (int ci = 0; ci < 3; ++ci) d[ci] = *reinterpret_cast<const int4*>(qrow + ci * cstride + (int64_t)ki * W);
-  };
-  // B: thread t moves column t >> 1, k half t & 1 (8 floats)
-  const int cb = tid >> 1, kh2 = tid & 1;
-  v4f bv[2];
-  auto load_b = [&](int kt) {
-    const int64_t n = n0 + cb;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      bv[u] = n < N ? *reinterpret_cast<const v4f*>(wt + n * K + kt * 16 + 8 * kh2 + 4 * u) : v4f{0, 0, 0, 0};
-  };
-  auto store_b = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) *reinterpret_cast<v4f*>(&sb[buf][cb * EQ_ROW + 8 * kh2 + 4 * u]) = bv[u];
-  };
-  // the 16 k values of k-tile sub of the kernel row: k_local -> p = (k_local & 1) * 8 + (k_local >> 1)
-  auto store_a = [&](int buf, auto SUB, const int4 (&d)[3]) __attribute__((always_inline)) {
-    constexpr int sub = decltype(SUB)::value;
-    float f[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int j = 16 * sub + e, kj = j / 3, c = j % 3;
-      const int w = (kj >> 2) == 0 ? d[c].x : (kj >> 2) == 1 ? d[c].y : (kj >> 2) == 2 ? d[c].z : d[c].w;
-      f[e] = ((float)(int)(int8_t)(w >> (8 * (kj & 3))) - zpf) * s;
-    }
-    float* dst = &sa[buf][tid * EQ_ROW];
-    *reinterpret_cast<v4f*>(dst) = v4f{f[0], f[2], f[4], f[6]};
-    *reinterpret_cast<v4f*>(dst + 4) = v4f{f[8], f[10], f[12], f[14]};
-    *reinterpret_cast<v4f*>(dst + 8) = v4f{f[1], f[3], f[5], f[7]};
-    *reinterpret_cast<v4f*>(dst + 12) = v4f{f[9], f[11], f[13], f[15]};
-  };
-  v16f acc[4][2], tot[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = tot[i][j][r] = 0.0f;
-  int blk = 0;
-  int64_t bend = kb.n > 0 ? kb.end[0] : -1;
-  load_px(0, px);
-  load_b(0);
-  store_a(0, std::integral_constant<int, 0>{}, px);
-  store_b(0);
-  __syncthreads();
-  auto step = [&](int kt, auto SUB) __attribute__((always_inline)) {
-    constexpr int sub = decltype(SUB)::value;
-    const int cur = kt & 1;
-    const bool more = kt + 1 < NKT;
-    if (more) {
-      load_b(kt + 1);
-      if constexpr (sub == 2) load_px((kt + 1) / 3, pxn);
-    }
-    v4f fa[4][2], fb[2][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float* src = &sa[cur][(wm * 128 + i * 32 + r32) * EQ_ROW + 8 * h];
-      fa[i][0] = *reinterpret_cast<const v4f*>(src);
-      fa[i][1] = *reinterpret_cast<const v4f*>(src + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float* src = &sb[cur][(wn * 64 + j * 32 + r32) * EQ_ROW + 8 * h];
-      fb[j][0] = *reinterpret_cast<const v4f*>(src);
-      fb[j][1] = *reinterpret_cast<const v4f*>(src + 4);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][kk >> 2][kk & 3], fb[j][kk >> 2][kk & 3], acc[i][j], 0, 0, 0);
-    if ((int64_t)kt * 16 + 16 == bend) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            tot[i][j][r] = tot[i][j][r] + acc[i][j][r];
-            acc[i][j][r] = 0.0f;
-          }
-      ++blk;
-      bend = blk < kb.n ? kb.end[blk] : -1;
-    }
-    if (more) {
-      if constexpr (sub == 2) {
-#pragma unroll
-        for (int ci = 0; ci < 3; ++ci) px[ci] = pxn[ci];
-      }
-      store_a(cur ^ 1, std::integral_constant<int, (sub + 1) % 3>{}, px);
-      store_b(cur ^ 1);
-    }
-    __syncthreads();
-  };
-  for (int ki = 0; ki < NKT / 3; ++ki) {
-    step(3 * ki, std::integral_constant<int, 0>{});
-    step(3 * ki + 1, std::integral_constant<int, 1>{});
-    step(3 * ki + 2, std::integral_constant<int, 2>{});
-  }
-  const int hwi = (int)ee.hw, Ni = (int)N, Mi = (int)M;
-  const float rhw = 1.0f / (float)hwi;
-  float bj[2];
-  int gnj[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    gnj[j] = (int)n0 + wn * 64 + j * 32 + r32;
-    bj[j] = gnj[j] < Ni ? ee.bias[gnj[j]] : 0.0f;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int gm = (int)m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (gm >= Mi) continue;
-      int im = (int)((float)gm * rhw);
-      im = im * hwi > gm ? im - 1 : im;
-      im = (im + 1) * hwi <= gm ? im + 1 : im;
-      const int co = (gm + im + 1) * Ni, po = (gm - im * hwi + 1) * Ni;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (gnj[j] < Ni) C[co + gnj[j]] = (tot[i][j][r] + bj[j]) + ee.pos[po + gnj[j]];
-    }
-}
-
 // class-token rows of the EMBED output: out[image][0][n] = cls[n] + pos[0][n]
 __global__ void k_embed_cls(const float* __restrict__ cls, const float* __restrict__ pos, float* __restrict__ out,
                             int64_t images, int64_t hw, int64_t n) {
@@ -1070,11 +918,9 @@ extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float
   const float zpf = (float)zp;
   // (a 3-stage LDS ring with the next k-tile's fragments read under the MFMAs measured 1.5 %
   // slower: 634 vs 625 us, profiles/r04_embed_ring_dropped.txt)
-  const char* e4 = getenv("NQK_EMBED_1WG");
-  if (N % 128 == 0 && !(e4 && atoi(e4) == 0)) {
-    hipLaunchKernelGGL(k_embed_q4, dim3((unsigned)(N / 128), (unsigned)((M + 255) / 256)), dim3(256), 0, stream(), q, wt,
-                       out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw});
-  } else if (N % 128 == 0) {
+  // (also dropped: one workgroup per CU, 256 x 128 tiles, one wave per SIMD — 768 vs 605 us,
+  // profiles/r04_embed_1wg_streams_dropped.txt)
+  if (N % 128 == 0) {
     hipLaunchKernelGGL(k_embed_q<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
                        wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw});
   } else {

@@ -11,7 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _run_both(B, H, T, zq, zk, zp, zv, zc, bw=8, seed=0):
+def _run_both(B, H, T, zq, zk, zp, zv, zc, bw=8, seed=0, s_p=1.0 / 255, s_qk=(0.031, 0.027)):
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray
     from numpy_quant.plan import EPI_PV, EPI_SCORES, _gemm
@@ -21,8 +21,8 @@ def _run_both(B, H, T, zq, zk, zp, zv, zc, bw=8, seed=0):
     q = rng.integers(lo, hi + 1, size=(B * H, T, Dh), dtype=np.int8)
     k = rng.integers(lo, hi + 1, size=(B * H, T, Dh), dtype=np.int8)
     v = rng.integers(lo, hi + 1, size=(B * H, T, Dh), dtype=np.int8)
-    s_q, s_k, s_v = np.float32(0.031), np.float32(0.027), np.float32(0.043)
-    s_p = np.float32(1.0 / 255)
+    s_q, s_k, s_v = np.float32(s_qk[0]), np.float32(s_qk[1]), np.float32(0.043)
+    s_p = np.float32(s_p)
     s_ctx = np.float32(0.017)
     div = 8.0
     dq, dk, dv = (DeviceArray.from_host(a.reshape(B * H * T, Dh)) for a in (q, k, v))
@@ -73,6 +73,17 @@ def test_attention_matches_three_launch_chain(T):
                                               (4096, -4096, 1024, -1024, 0, 8), (-9, 2, -8, 1, 3, 4)])
 def test_attention_zero_points_and_bit_widths(zq, zk, zp, zv, zc, bw):
     f, u = _run_both(1, 12, 197, zq, zk, zp, zv, zc, bw=bw, seed=abs(zq) + bw)
+    np.testing.assert_array_equal(f, u)
+
+
+@pytest.mark.parametrize("s_p,zp,s_qk", [(8.051e-05, -142, (0.02, 0.0225)), (2.3e-4, -131, (0.011, 0.009)),
+                                         (1.0 / 255, -128, (0.002, 0.003))])
+def test_attention_calibrated_softmax_scales(s_p, zp, s_qk):
+    """Parameters like the bench model's calibration (its last layer: s_p 8.05e-5, zp_p -142,
+    scores within a few units): the P quantize clamps at the bottom (zp < -128), most P
+    values are a few units, so the per-element filter margin decides nearly every element
+    on the fast path; small scores keep every exp on the exponent-add path."""
+    f, u = _run_both(4, 12, 197, zq=0, zk=-6, zp=zp, zv=-14, zc=-11, seed=int(zp) + 1000, s_p=s_p, s_qk=s_qk)
     np.testing.assert_array_equal(f, u)
 
 
