@@ -250,6 +250,10 @@ typedef struct nqk_epilogue {
   float lut_k[5];                       /* nqk_gelu_lut_build, its bucket coordinate and   */
   int32_t lut_n;                        /* entry count; k_pg then looks the GELU chain's   */
                                         /* output bytes up instead of computing them       */
+  int32_t col_l1max;                    /* optional: max over columns of sum_k |Bt[n][k]|  */
+                                        /* (0: unknown); |acc| <= 2^(bw-1) col_l1max then  */
+                                        /* bounds the f32-exactness test more tightly than */
+                                        /* 2^(2bw-2) K (FFN-down at K = 3072)              */
 } nqk_epilogue;
 /* int8 MFMA GEMM C = A . Bt^T (layouts as nqk_qgemm_i8) with a fused epilogue:
  *   QKV    model.py MatMul -> Add(bias) -> Reshape -> Transpose -> quantize, 3 groups

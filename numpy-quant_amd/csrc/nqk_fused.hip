@@ -1957,15 +1957,20 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     // f32 epilogue arithmetic when every |acc - col term| < 2^24 (int8 operands:
     // |acc| <= 2^14 K) and the output zero points are exact in f32 with room to spare
     const double cmax = params->col_absmax > 0 ? (double)params->col_absmax : 128.0 * (double)K;
+    // |sum_k a b| <= 2^14 K for int8 operands, or 128 max_n sum_k |b| when the host gave the
+    // weights' largest column L1 norm (|a| <= 128)
+    const double abound = params->col_l1max > 0 && !getenv("NQK_NO_L1")
+                              ? std::min(16384.0 * (double)K, 128.0 * (double)params->col_l1max)
+                              : 16384.0 * (double)K;
     const int ng = epi == EPI_QKV ? 3 : 1;
     bool zp_small = true;
     for (int g = 0; g < ng; ++g) zp_small = zp_small && params->zp_out[g] >= -(1 << 20) && params->zp_out[g] <= (1 << 20);
     const bool f32x = i32 && (epi == EPI_QKV || (epi == EPI_GELU && e.gelu_filter)) && zp_small &&
-                      16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
+                      abound + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
     const bool use_pp = pp && !params->b_packed;
     // the persistent 16x16x64 GEMM (nqk_pgemm.hip) where it takes the case
     if (params->bt_pg != nullptr) {
-      const bool f32x_r = i32 && epi == EPI_RESID && 16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
+      const bool f32x_r = i32 && epi == EPI_RESID && abound + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
       const int rc = pg_launch(epi, a, params->bt_pg, M, N, K, lda, params, f32x || f32x_r);
       if (rc < 0) return rc;
       if (rc > 0) {
@@ -1977,7 +1982,7 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     // GELU with NQK_PROJ_GELU=1 and the residual epilogues with NQK_PROJ_RESID=1 (faster
     // alone, not inside the two-stream forward, DESIGN.md "Projection GEMM variants");
     // NQK_NO_PROJ=1 keeps the one-tile-per-workgroup kernel everywhere
-    const bool f32x_r = i32 && epi == EPI_RESID && 16384.0 * (double)K + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
+    const bool f32x_r = i32 && epi == EPI_RESID && abound + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
     const bool proj_shape = params->b_packed && i32 && params->colterm != nullptr && M >= 256 && (M % 256 == 0 || epi != EPI_RESID) && N % GBN == 0 &&
                             (K == 768 || K == 3072) && (double)M * N * 4.0 < 4294967295.0 && (double)M * lda < 4294967295.0 &&
                             !getenv("NQK_NO_PROJ") &&

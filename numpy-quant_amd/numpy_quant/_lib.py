@@ -34,7 +34,8 @@ class Epilogue(ctypes.Structure):
                 ("out", ctypes.c_void_p * 3), ("bias", ctypes.c_void_p), ("resid", ctypes.c_void_p),
                 ("div", ctypes.c_float), ("add1", ctypes.c_float), ("mul2", ctypes.c_float),
                 ("b_packed", ctypes.c_int32), ("colterm", ctypes.c_void_p), ("bt_pg", ctypes.c_void_p),
-                ("gelu_lut", ctypes.c_void_p), ("lut_k", ctypes.c_float * 5), ("lut_n", ctypes.c_int32)]
+                ("gelu_lut", ctypes.c_void_p), ("lut_k", ctypes.c_float * 5), ("lut_n", ctypes.c_int32),
+                ("col_l1max", ctypes.c_int32)]
 
 
 class Attention(ctypes.Structure):

@@ -582,6 +582,10 @@ class FusedLayer:
         # max |column sum| of each weight: lets the GEMM epilogues prove f32 exactness
         self.cmax = {k: _absmax(c) for k, c in (("qkv", self.col_qkv), ("o", self.col_o), ("1", self.col_1),
                                                  ("2", self.col_2))}
+        # max column L1 norm of each weight: a tighter |acc| bound for the same proof (FFN-down,
+        # K = 3072, then dequantizes in f32 too)
+        self.l1max = {k: _l1max(b) for k, b in (("qkv", self.bt_qkv), ("o", self.bt_o), ("1", self.bt_1),
+                                                 ("2", self.bt_2))}
         # int32 zero-point column terms col * zp_a of each GEMM (the persistent GEMM's
         # per-column constant; None where they do not fit int32)
         self.ct = {k: _colterm(c, _zp(p)) for k, c, p in (("qkv", self.col_qkv, self.p_ln1), ("o", self.col_o, self.p_ctx),
@@ -688,7 +692,7 @@ class FusedLayer:
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D, col=self.col_qkv.ptr,
-                      col_absmax=self.cmax["qkv"], colterm=_ptr(self.ct["qkv"]),
+                      col_absmax=self.cmax["qkv"], col_l1max=self.l1max["qkv"], colterm=_ptr(self.ct["qkv"]),
                       s_acc=[_f32(s_a * np.float32(self.s_w[r])) for r in "qkv"],
                       s_out=[_f32(self.p_head[r].scale) for r in "qkv"],
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
@@ -711,7 +715,7 @@ class FusedLayer:
         else:
             self._attention_unfused(w, nb, T, Tp, H, Dh, D)  # whole batch only (i0 == 0)
         # 7) output projection + bias + residual
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr, col_absmax=self.cmax["o"],
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr, col_absmax=self.cmax["o"], col_l1max=self.l1max["o"],
                       colterm=_ptr(self.ct["o"]),
                       s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
                       resid=x.ptr, out=[x1.ptr])
@@ -719,7 +723,7 @@ class FusedLayer:
         # 8) LN2 + quantize
         _ln_quant(x1, self.g2, self.be2, ln2q, Mrows, D, self.eps2, self.p_ln2, bw)
         # 9) FFN up + bias + GELU + quantize
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr, col_absmax=self.cmax["1"],
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr, col_absmax=self.cmax["1"], col_l1max=self.l1max["1"],
                       colterm=_ptr(self.ct["1"]),
                       s_acc=[_f32(np.float32(self.p_ln2.scale) * np.float32(self.s_w1))], bias=self.bias_1.ptr,
                       s_out=[_f32(self.p_h.scale)], zp_out=[_zp(self.p_h)], out=[hh.ptr],
@@ -730,7 +734,7 @@ class FusedLayer:
                 e.lut_k[j] = kv
         _gemm(EPI_GELU, ln2q, self._b(e, "1", self.bt_1), 1, Mrows, F, D, D, D, None, 0, 0, e)
         # 10) FFN down + bias + residual
-        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr, col_absmax=self.cmax["2"],
+        e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_h), col=self.col_2.ptr, col_absmax=self.cmax["2"], col_l1max=self.l1max["2"],
                       colterm=_ptr(self.ct["2"]),
                       s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
                       resid=x1.ptr, out=[x2.ptr])
@@ -796,6 +800,13 @@ def _colterm(col, zpa):
     if c.size and (c.min() < -2 ** 31 or c.max() >= 2 ** 31):
         return None
     return DeviceArray.from_host(c.astype(np.int32))
+
+
+def _l1max(bt) -> int:
+    """max over rows n of sum_k |Bt[n][k]| (int32-clamped; >= 1: 0 would mean unknown)."""
+    h = np.abs(bt.to_host().astype(np.int64))
+    v = int(h.sum(axis=1).max()) if h.size else 1
+    return max(1, min(v, 2 ** 31 - 1))
 
 
 def _absmax(col) -> int:

@@ -17,7 +17,7 @@ def _last_kernel():
     return _lib.load().nqk_qgemm_last_kernel()
 
 
-def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, kernel=2, bw=8):
+def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, kernel=2, bw=8, l1=False):
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray
     from numpy_quant.plan import EPI_GELU, EPI_QKV, EPI_RESID, _gemm, _pack_b, _pack_pg
@@ -45,6 +45,8 @@ def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, ker
     e.zp_flags, e.bit_width = _lib.ZP_COL, bw
     e.zpa, e.col, e.col_absmax = zpa, col.ptr, int(np.abs(col_h).max())
     e.bias, e.b_packed, e.colterm = bias.ptr, kind, colterm.ptr
+    if l1:  # the weights' largest column L1 norm: the tighter |acc| bound of the f32 proof
+        e.col_l1max = int(np.abs(bt_h.astype(np.int64)).sum(axis=1).max())
     e.bt_pg = pg.ptr if use_pg else None
     sa = 1.3e-4
     if epi == EPI_QKV:
@@ -161,4 +163,17 @@ def test_pg_gemm_int4_equals_big_tile(epi_name, M, N, K, s_out_scale, no_f32x, m
     k1, got, _ = _run(epi_name, M, N, K, s_out_scale, True, no_f32x, monkeypatch, seed, 1, bw=4)
     assert (k0, k1) == (1, 4), (k0, k1)
     for x, y in zip(ref, got):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("M,seed", [(128 * 197, 11), (256 * 197, 12), (300, 13)])
+def test_pg_resid_k3072_f32_dequant_from_column_l1_bound(M, seed, monkeypatch):
+    """FFN-down (K = 3072): 2^14 K exceeds 2^24, so without more information the residual
+    epilogue dequantizes in f64; with the weights' largest column L1 norm (col_l1max) the
+    bound 128 L1 + |zpa| cmax < 2^24 proves the f32 dequantize exact.  Both runs of k_pg
+    (the f32 one by the L1 bound, the f64 one with NQK_NO_F32X=1) are bit-identical."""
+    k1, f32, _ = _run("resid", M, 768, 3072, 1.0, True, False, monkeypatch, seed, 1, l1=True)
+    k2, f64, _ = _run("resid", M, 768, 3072, 1.0, True, True, monkeypatch, seed, 1, l1=True)
+    assert (k1, k2) == (4, 4), (k1, k2)
+    for x, y in zip(f32, f64):
         np.testing.assert_array_equal(x, y)
