@@ -199,7 +199,7 @@ struct PgEpi {
   float sacc[3];      // dequant scale per column group
   float rsf[3];       // RN32(1 / s_out)
   float c1[3];        // RN32(sacc * rsf)            (QKV fast path)
-  float k1[3];        // |c1| 2^-21                  (QKV filter: rounding error per |v|)
+  float k1[3];        // |c1| 6.25 2^-24             (QKV filter: rounding error per |v|)
   float zp128[3];     // zp_out + 128 (f32)        (QKV: v_rndne + v_cvt_pk_u8 rounding)
   float qlo[3], qhi[3], magic[3];  // lo - zp, hi - zp, 1.5 2^23 + zp (GELU: pg_round2)
   float s_out[3];
@@ -343,6 +343,15 @@ __device__ __forceinline__ void gelu_fast2x2(v2f h0, v2f h1, v2f& g0, v2f& g1) {
 // Q_LIM = (0.5 - 2^-126)(1 - 2^-23) rounded down: a rounded fma measure below it keeps the
 // exact one below 0.5 - 2^-126 (nqk_fused.hip quant_filter)
 constexpr float PG_QLIM = 0x1.fffffcp-2f;
+// QKV filter margin (round 4): |u - t| <= 6 units (2^-24) of |v c1| + 5 of |c2| to first order —
+// the roundings of c1 = RN(sacc rsf), rsf = RN(1/s) and the fma on the fast side, of v sacc,
+// + bias and / s_out on the reference's — so 6.25 and 5.25 units (round 3 used 8 and 16)
+#ifndef NQK_PG_QK1
+#define NQK_PG_QK1 0x1.9p-22f  // 6.25 2^-24 per |v c1|
+#endif
+#ifndef NQK_PG_QKC2
+#define NQK_PG_QKC2 0x1.5p-22f  // 5.25 2^-24 per |c2|
+#endif
 
 
 // B4: int4 weights (every value in [-8, 7]) as the nibble image of nqk_pack_pg4: a stage's
@@ -533,7 +542,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
           c2[q] = bias[q] * rsf;
           cm = __builtin_fmaxf(cm, __builtin_fabsf(c2[q]));
         }
-        lim = (PG_QLIM - cm * 0x1p-20f) - 0x1p-22f;  // conservative: every rounding down
+        lim = (PG_QLIM - cm * NQK_PG_QKC2) - 0x1p-22f;  // conservative: every rounding down
       } else {
         lim = e.g_lim;
       }
@@ -1096,7 +1105,7 @@ k_pg2(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N,
           ecol[q] = b;
         }
       }
-      t.lim = EPI == PG_QKV ? (PG_QLIM - cm * 0x1p-20f) - 0x1p-22f : e.g_lim;
+      t.lim = EPI == PG_QKV ? (PG_QLIM - cm * NQK_PG_QKC2) - 0x1p-22f : e.g_lim;
     }
     return t;
   };
@@ -1455,7 +1464,7 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     e.zp_out[g] = (double)p->zp_out[gg];
     e.rsf[g] = s_out != 0.0f ? (float)(1.0 / (double)s_out) : 0.0f;
     e.c1[g] = e.sacc[g] * e.rsf[g];
-    e.k1[g] = __builtin_fabsf(e.c1[g]) * 0x1p-21f;
+    e.k1[g] = __builtin_fabsf(e.c1[g]) * NQK_PG_QK1;
     e.zp128[g] = (float)p->zp_out[gg] + 128.0f;
     e.qlo[g] = (float)qlo - (float)p->zp_out[gg];
     e.qhi[g] = (float)qhi - (float)p->zp_out[gg];
