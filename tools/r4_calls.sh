@@ -227,7 +227,15 @@ r4_k() {
 
 }
 
+r4_l() {
+  # operand-delivery probe: k_pg without its B pieces (-DNQK_PG_DIAG=128), without its A pieces
+  # (256), without both (4); wrong results, timings only
+  rm -f gpurun_out/l.status
+  timeout -k 10 300 env PGM_LIBS=nob=tools/diag/libnqk_nob.so,noa=tools/diag/libnqk_noa.so,noab=tools/diag/libnqk_noab.so PGM_ROUNDS=3 python -u tools/pg_micro.py > gpurun_out/l_pg_operands.txt 2>&1
+  echo "== pg_operands rc=$?" >> gpurun_out/l.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l}" >&2; exit 2 ;;
 esac
