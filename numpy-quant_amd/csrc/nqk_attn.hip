@@ -39,6 +39,23 @@
 #ifndef NQK_ATTN_PREL
 #define NQK_ATTN_PREL 1  // 1: P filter margin per element (|tf| 2^-21) instead of the row's (kpf 2^-20)
 #endif
+// P filter margins (NQK_ATTN_PREL), per element: the reference's t = RN(RN(e / tot) / s_p) is within
+// (2u + u^2)|x| of x = e / (tot s_p) (u = 2^-24), kpf = RN(rtot rs_p) within (u + 3 2^-53)|x| / e.
+// Clamp-free path: r = rint(e kpf) exactly, so |t - e kpf| <= 3.0001 u |x| <= 4.5002 u |r| for |r| >= 1
+// (|x| <= |r| + 0.5 + ...; r = 0: 1.5 u, under the limit's 2 u): margin 4.75 u |r|.
+// Clamped path: tf = RN(e kpf) adds u, |t - tf| <= 4.0001 u |x| <= 4.002 u |tf|: margin 4.125 u |tf|.
+// Both then pass only below 0.5 - 2u, which also takes dd's and the measure's own roundings
+// (0.25 u each).  (Round 3 used 8 u for both: about twice the fallbacks.)
+#ifndef NQK_ATTN_PM_R
+#define NQK_ATTN_PM_R 0x1.3p-22f
+#endif
+#ifndef NQK_ATTN_PM_T
+#define NQK_ATTN_PM_T 0x1.08p-22f
+#endif
+#ifndef NQK_ATTN_PKL
+#define NQK_ATTN_PKL 0  // 1: clamped path tf = RN(e kpf + RN(e kpl)) (kpf + kpl = the double product):
+                        // |t - tf| <= 3.001 u |tf|, margin 3.125 u |tf| (A/B variant)
+#endif
 #ifndef NQK_ATTN_PSUM
 #define NQK_ATTN_PSUM 1  // 1: the pairwise-sum accumulators as packed pairs (v_pk_add_f32)
 #endif
@@ -446,7 +463,10 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     }
     const float tot = n2 ? leaf[0] + leaf[1] : leaf[0];
     const double rtot = 1.0 / (double)tot;
-    const float kpf = (float)(rtot * a.rs_p);  // t = e / tot / s_p within |t| 2^-22 of e * kpf
+    const double kpd = rtot * a.rs_p;
+    const float kpf = (float)kpd;  // t = e / tot / s_p within |t| 2^-22 of e * kpf
+    const float kpl = NQK_ATTN_PKL ? (float)(kpd - (double)kpf) : 0.0f;
+    constexpr float PM_T = NQK_ATTN_PKL ? 0x1.9p-23f : NQK_ATTN_PM_T;
     // the filter's bound for the whole row (|tf| <= kpf (1 + 2^-23)), with margin
     const float plim = 0.5f - 2.0f * __builtin_fmaf(kpf, 0x1p-21f, 0x1p-126f);
     const float zp128 = a.zp_p_f + 128.0f, lo128 = a.lo_f + 128.0f, hi128 = a.hi_f + 128.0f;
@@ -460,7 +480,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     // the exact product (one rounding fewer than tf = RN(e kpf), so still within |t| 2^-22 of
     // t), dd = RN(e kpf - (s - pmagic)) within 2^-25 of the exact distance (the limit takes
     // 2^-24 off for it)
-    const bool pq_nc = NQK_ATTN_PQ2 && pqlo <= 0.0f && __all(kpf <= pqhi);
+    // (diagnostic 512: the clamp-free path on every row, wrong results where a clamp is reached)
+    const bool pq_nc = NQK_ATTN_PQ2 && ((NQK_ATTN_DIAG & 512) != 0 || (pqlo <= 0.0f && __all(kpf <= pqhi)));
     const float plim2 = plim - 0x1p-24f;
     if (!pq_nc) NQK_ATTN_COUNT(1);
     v16i acc2[2];
@@ -494,13 +515,13 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             const v2f_t dd0 = __builtin_elementwise_fma(e0, k2, -(s0 - m2));
             const v2f_t dd1 = __builtin_elementwise_fma(e1, k2, -(s1 - m2));
             if constexpr (NQK_ATTN_PREL) {
-              // |t - e kpf| <= 3 2^-24 |t|: the margin 2^-21 |r| (r = the rounded value; at r = 0
-              // the limit itself covers it), the limit 0.5 - 2^-22 absorbs dd's own rounding
+              // |t - e kpf| <= 3 2^-24 |x|: the margin NQK_ATTN_PM_R |r| (r = the rounded value; at
+              // r = 0 the limit itself covers it), the limit 0.5 - 2^-23 absorbs dd's own rounding
               const v2f_t r0 = s0 - m2, r1 = s1 - m2;
-              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(r0[0]), 0x1p-21f, __builtin_fabsf(dd0[0])),
-                                                             __builtin_fmaf(__builtin_fabsf(r0[1]), 0x1p-21f, __builtin_fabsf(dd0[1]))));
-              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(r1[0]), 0x1p-21f, __builtin_fabsf(dd1[0])),
-                                                             __builtin_fmaf(__builtin_fabsf(r1[1]), 0x1p-21f, __builtin_fabsf(dd1[1]))));
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(r0[0]), NQK_ATTN_PM_R, __builtin_fabsf(dd0[0])),
+                                                             __builtin_fmaf(__builtin_fabsf(r0[1]), NQK_ATTN_PM_R, __builtin_fabsf(dd0[1]))));
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(r1[0]), NQK_ATTN_PM_R, __builtin_fabsf(dd1[0])),
+                                                             __builtin_fmaf(__builtin_fabsf(r1[1]), NQK_ATTN_PM_R, __builtin_fabsf(dd1[1]))));
             } else {
               worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd0[0]), __builtin_fabsf(dd0[1])));
               worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd1[0]), __builtin_fabsf(dd1[1])));
@@ -515,7 +536,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             }
             dw[qq] = (int)w;
           }
-          if (__builtin_expect(__any(!(worst < (NQK_ATTN_PREL ? 0x1.fffff8p-2f : plim2))), 0)) {
+          // (diagnostic 256: the exact fallbacks skipped)
+          if ((NQK_ATTN_DIAG & 256) == 0 && __builtin_expect(__any(!(worst < (NQK_ATTN_PREL ? 0x1.fffff8p-2f : plim2))), 0)) {
             NQK_ATTN_COUNT(2);
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) {
@@ -526,7 +548,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
                 const float x = e[c][4 * qq + j];
                 const float rr = __builtin_fmaf(x, kpf, pmagic) - pmagic;
                 const float d = __builtin_fmaf(x, kpf, -rr);
-                if (!(NQK_ATTN_PREL ? __builtin_fmaf(__builtin_fabsf(rr), 0x1p-21f, __builtin_fabsf(d)) < 0x1.fffff8p-2f
+                if (!(NQK_ATTN_PREL ? __builtin_fmaf(__builtin_fabsf(rr), NQK_ATTN_PM_R, __builtin_fabsf(d)) < 0x1.fffff8p-2f
                                     : __builtin_fabsf(d) < plim2)) {
                   const int qv = n < T ? quant_w(div_rc_w(x, rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) : 0;
                   dw[qq] = (int)(((uint32_t)dw[qq] & ~(0xffu << (8 * j))) | ((uint32_t)(qv & 0xff) << (8 * j)));
@@ -545,17 +567,19 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
             // pairs: one v_pk_mul for tf, the clamp / magic-number rounding + byte pack of
             // round_magic2 / pack4_low (nqk_numerics.h), |dd| into the tile's worst
             v2f_t dd0, dd1;
-            const v2f_t tf0 = v2f_t{e[c][4 * qq], e[c][4 * qq + 1]} * v2f_t{kpf, kpf};
-            const v2f_t tf1 = v2f_t{e[c][4 * qq + 2], e[c][4 * qq + 3]} * v2f_t{kpf, kpf};
+            const v2f_t ea = v2f_t{e[c][4 * qq], e[c][4 * qq + 1]}, eb = v2f_t{e[c][4 * qq + 2], e[c][4 * qq + 3]};
+            const v2f_t k2 = v2f_t{kpf, kpf}, kl2 = v2f_t{kpl, kpl};
+            const v2f_t tf0 = NQK_ATTN_PKL ? __builtin_elementwise_fma(ea, k2, ea * kl2) : ea * k2;
+            const v2f_t tf1 = NQK_ATTN_PKL ? __builtin_elementwise_fma(eb, k2, eb * kl2) : eb * k2;
             const v2f_t s0 = round_magic2(tf0, pqlo, pqhi, pmagic, dd0);
             const v2f_t s1 = round_magic2(tf1, pqlo, pqhi, pmagic, dd1);
             if constexpr (NQK_ATTN_PREL) {
-              // |t - tf| <= 4 2^-24 |t|: the margin 2^-21 |tf| per element (clamped elements:
+              // |t - tf| <= 4 2^-24 |x|: the margin NQK_ATTN_PM_T |tf| per element (clamped elements:
               // dd = 0, and the clamp decides them either way)
-              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(tf0[0]), 0x1p-21f, __builtin_fabsf(dd0[0])),
-                                                             __builtin_fmaf(__builtin_fabsf(tf0[1]), 0x1p-21f, __builtin_fabsf(dd0[1]))));
-              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(tf1[0]), 0x1p-21f, __builtin_fabsf(dd1[0])),
-                                                             __builtin_fmaf(__builtin_fabsf(tf1[1]), 0x1p-21f, __builtin_fabsf(dd1[1]))));
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(tf0[0]), PM_T, __builtin_fabsf(dd0[0])),
+                                                             __builtin_fmaf(__builtin_fabsf(tf0[1]), PM_T, __builtin_fabsf(dd0[1]))));
+              worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(tf1[0]), PM_T, __builtin_fabsf(dd1[0])),
+                                                             __builtin_fmaf(__builtin_fabsf(tf1[1]), PM_T, __builtin_fabsf(dd1[1]))));
             } else {
               worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd0[0]), __builtin_fabsf(dd0[1])));
               worst = __builtin_fmaxf(worst, __builtin_fmaxf(__builtin_fabsf(dd1[0]), __builtin_fabsf(dd1[1])));
@@ -585,7 +609,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
           dw[qq] = (int)(packed ^ 0x80808080u);
         }
         const bool prel = NQK_ATTN_PREL && NQK_ATTN_PK;
-        if (__builtin_expect(__any(!(worst < (prel ? 0x1.fffff8p-2f : plim))), 0)) {
+        if ((NQK_ATTN_DIAG & 256) == 0 && __builtin_expect(__any(!(worst < (prel ? 0x1.fffff8p-2f : plim))), 0)) {
           NQK_ATTN_COUNT(2);
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq) {
@@ -593,10 +617,11 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int n = c * 32 + 8 * qq + 4 * h + j;
-              const float tf = e[c][4 * qq + j] * kpf;
+              const float ej = e[c][4 * qq + j];
+              const float tf = NQK_ATTN_PKL ? __builtin_fmaf(ej, kpf, ej * kpl) : ej * kpf;
               const float cf = prel ? __builtin_amdgcn_fmed3f(tf, pqlo, pqhi) : tf;  // (the clamp as in the fast path)
               const float dv = __builtin_fabsf(cf - __builtin_rintf(cf));
-              if (!(prel ? __builtin_fmaf(__builtin_fabsf(tf), 0x1p-21f, dv) < 0x1.fffff8p-2f : dv < plim)) {
+              if (!(prel ? __builtin_fmaf(__builtin_fabsf(tf), PM_T, dv) < 0x1.fffff8p-2f : dv < plim)) {
                 const int qv = n < T ? quant_w(div_rc_w(e[c][4 * qq + j], rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) : 0;
                 dw[qq] = (int)(((uint32_t)dw[qq] & ~(0xffu << (8 * j))) | ((uint32_t)(qv & 0xff) << (8 * j)));
               }

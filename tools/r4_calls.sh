@@ -235,7 +235,51 @@ r4_l() {
   echo "== pg_operands rc=$?" >> gpurun_out/l.status
 }
 
+
+r4_m() {
+  # round-4 call M: where the attention's time goes on the bench's own data — diagnostic builds
+  # (tools/gemm_diag.sh with SRC=nqk_attn, NQK_ATTN_DIAG bits: 1 no V^T staging, 2 no exp,
+  # 4 no P quantize, 8 no score MFMAs, 16 no context quantize, 32 no PV MFMAs, 64 no K/V loads,
+  # 256 no P exact fallbacks, 512 the clamp-free P path everywhere) timed beside the main build
+  rm -f gpurun_out/m.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/m.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  L=""
+  for n in a1 a2 a4 a8 a16 a32 a64 a256 a512 a768; do L="$L,$n=tools/diag/libnqk_$n.so"; done
+  timeout -k 10 400 env AM_LIBS="${L#,}" python -u tools/attn_real.py > gpurun_out/m_attn_real.txt 2>&1
+  step attn_real $?
+  echo done >> gpurun_out/m.status
+}
+
+r4_n() {
+  # round-4 call N: the attention's P filter margins from the error bound (4.75 u |r| clamp-free,
+  # 4.125 u |tf| clamped, instead of 8 u) and the double-float kpf variant (apkl, 3.125 u):
+  # parity, timing and slow-path counts on the bench's data (aold = the previous build,
+  # *stat = NQK_ATTN_DIAG 128 counters), whole-bench A/B main vs aold / apkl
+  rm -f gpurun_out/n.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/n.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_kernels.py tests/test_gpu_b256.py -x -q --timeout 300 --timeout-method thread > gpurun_out/n_tests.log 2>&1
+  step tests $?
+  timeout -k 10 400 env AM_LIBS=aold=tools/diag/libnqk_aold.so,apkl=tools/diag/libnqk_apkl.so,astat=tools/diag/libnqk_astat.so,aoldstat=tools/diag/libnqk_aoldstat.so,apklstat=tools/diag/libnqk_apklstat.so python -u tools/attn_real.py > gpurun_out/n_attn_real.txt 2>&1
+  step attn_real $?
+  AB_LIBS="main aold apkl" AB_REPS=2 OUT=n bash tools/ab.sh
+  step ab $?
+  echo done >> gpurun_out/n.status
+}
+
+r4_o() {
+  # round-4 call O: instruction-cache counters per kernel over one B = 256 forward and the
+  # attention timing loop (tools/attn_real.py); the attention kernel's code is 66 KB
+  rm -f gpurun_out/o.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/o.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  rm -rf gpurun_out/pmc_ic
+  timeout -s KILL 300 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --kernel-trace -d gpurun_out/pmc_ic -o run --output-format csv -- python -u tools/attn_real.py > gpurun_out/o_pmc_ic.log 2>&1
+  step pmc_ic $?
+  python tools/pmc_kernels.py gpurun_out/pmc_ic --by-grid > gpurun_out/o_pmc_ic.txt 2>&1
+  step table $?
+  echo done >> gpurun_out/o.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k|l) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o}" >&2; exit 2 ;;
 esac
