@@ -279,7 +279,19 @@ r4_o() {
   echo done >> gpurun_out/o.status
 }
 
+r4_p() {
+  # round-4 call P: the attention's P exact fallbacks as one loop per tile over the failed
+  # elements (NQK_ATTN_FBL=1, code 66 -> 54 KB) vs per element (afbl0): parity, bench-data timing
+  rm -f gpurun_out/p.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/p.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_kernels.py tests/test_gpu_b256.py -x -q --timeout 300 --timeout-method thread > gpurun_out/p_tests.log 2>&1
+  step tests $?
+  timeout -k 10 400 env AM_LIBS=afbl0=tools/diag/libnqk_afbl0.so python -u tools/attn_real.py > gpurun_out/p_attn_real.txt 2>&1
+  step attn_real $?
+  echo done >> gpurun_out/p.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p}" >&2; exit 2 ;;
 esac
