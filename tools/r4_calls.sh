@@ -291,7 +291,45 @@ r4_p() {
   echo done >> gpurun_out/p.status
 }
 
+r4_q() {
+  # round-4 call Q: the QKV and GELU-table epilogues without packed f32 instructions
+  # (NQK_PG_NOPK=1; MI355X_MICROARCH.md: a v_pk_fma_f32 beside MFMAs costs more than two
+  # v_fma_f32): projection-GEMM micro and whole-bench A/B (the bench verifies every row)
+  rm -f gpurun_out/q.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/q.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 300 env PGM_LIBS=nopk=tools/diag/libnqk_nopk.so PGM_SHAPES=qkv,up PGM_ROUNDS=3 python -u tools/pg_micro.py > gpurun_out/q_pg_micro.txt 2>&1
+  step pg_micro $?
+  AB_LIBS="main nopk" AB_REPS=2 OUT=q bash tools/ab.sh
+  step ab $?
+  echo done >> gpurun_out/q.status
+}
+
+r4_r() {
+  # round-4 call R: which k_pg epilogue of the unpacked build (NQK_PG_NOPK=1) differs — the
+  # projection-GEMM parity tests with tools/diag/libnqk_nopk.so in place of the library
+  # (on the box's copy of the tree only)
+  rm -f gpurun_out/r.status
+  cp tools/diag/libnqk_nopk.so numpy-quant_amd/numpy_quant/libnqk.so
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_pgemm.py tests/test_gpu_glut.py -q -rf --timeout 300 --timeout-method thread > gpurun_out/r_tests.log 2>&1
+  echo "== tests rc=$?" >> gpurun_out/r.status
+}
+
+r4_s() {
+  # round-4 call S: the QKV epilogue unpacked (NQK_PG_NOPK=1, now the default; the unpacked GELU
+  # table epilogue of call Q wrote wrong bytes and is not used) against the packed build (qkvpk),
+  # and the residual epilogue unpacked as well (rnopk): parity, micro, whole-bench A/B
+  rm -f gpurun_out/s.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/s.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 700 python -u -m pytest tests/test_gpu_pgemm.py tests/test_gpu_glut.py tests/test_gpu_b256.py -x -q --timeout 300 --timeout-method thread > gpurun_out/s_tests.log 2>&1
+  step tests $?
+  timeout -k 10 300 env PGM_LIBS=qkvpk=tools/diag/libnqk_qkvpk.so,rnopk=tools/diag/libnqk_rnopk.so PGM_SHAPES=qkv,out,down PGM_ROUNDS=3 python -u tools/pg_micro.py > gpurun_out/s_pg_micro.txt 2>&1
+  step pg_micro $?
+  AB_LIBS="main qkvpk rnopk" AB_REPS=2 OUT=s bash tools/ab.sh
+  step ab $?
+  echo done >> gpurun_out/s.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s}" >&2; exit 2 ;;
 esac
