@@ -329,7 +329,23 @@ r4_s() {
   echo done >> gpurun_out/s.status
 }
 
+r4_t() {
+  # round-4 call T: the attention's element pairs as two scalar instructions instead of v_pk_*
+  # (NQK_ATTN_UNPK bits: 1 exp, 2 P quantize, 4 score dequantize, 8 context quantize, 15 all;
+  # ps0 = NQK_ATTN_PSUM=0, the pairwise sums unpacked): the exhaustive exp test (covers the
+  # unpacked exp), parity, timing on the bench's data
+  rm -f gpurun_out/t.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/t.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_attention.py tests/test_gpu_b256.py -x -q --timeout 300 --timeout-method thread > gpurun_out/t_tests.log 2>&1
+  step tests $?
+  L=""
+  for n in u1 u2 u4 u8 u15 ps0; do L="$L,$n=tools/diag/libnqk_$n.so"; done
+  timeout -k 10 400 env AM_LIBS="${L#,}" python -u tools/attn_real.py > gpurun_out/t_attn_real.txt 2>&1
+  step attn_real $?
+  echo done >> gpurun_out/t.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t}" >&2; exit 2 ;;
 esac
