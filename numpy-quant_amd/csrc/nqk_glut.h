@@ -43,7 +43,10 @@ __device__ __forceinline__ float glut_u(float h, const GLutK& k) {
 // byte B of pk := (h >= thr) ? info[23:16] : info[7:0], the other bytes kept, and the lanes
 // whose h lies in the entry's window OR-ed into `slow`: v_cmp + one SDWA v_cndmask that
 // selects a word of info and writes one byte of pk, v_sub + an SDWA compare with info[15:8],
-// s_or_b64 (a VALU-written SGPR read by SALU: interlocked, like v_cmp -> s_and_saveexec)
+// s_or_b64 (a VALU-written SGPR read by SALU: interlocked, like v_cmp -> s_and_saveexec).
+// The s_or_b64 writes SCC, so "scc" is a clobber: without it the compiler kept an s_cselect's
+// SCC live across the block, and a build that scheduled one there (the unpacked epilogue of
+// round-4 call Q / U) stored through a zero-size descriptor
 template <int B>
 __device__ __forceinline__ uint32_t glut_sel(uint32_t pk, float h, uint32_t thr, uint32_t info, uint64_t& slow) {
   static_assert(B >= 0 && B < 4, "byte");
@@ -58,7 +61,7 @@ __device__ __forceinline__ uint32_t glut_sel(uint32_t pk, float h, uint32_t thr,
       "s_or_b64 %[s], %[s], %[m]"                                                                                \
       : [pk] "+v"(pk), [d] "=&v"(d), [m] "=&s"(m), [s] "+s"(slow)                                                  \
       : [h] "v"(h), [t] "v"(thr), [i] "v"(info)                                                                  \
-      : "vcc")
+      : "vcc", "scc")
   if constexpr (B == 0) NQK_GLUT_SEL("BYTE_0");
   else if constexpr (B == 1) NQK_GLUT_SEL("BYTE_1");
   else if constexpr (B == 2) NQK_GLUT_SEL("BYTE_2");

@@ -87,6 +87,28 @@ __device__ __forceinline__ float np_expf_nonpos(float x) {
 // reduction.  Equal to np_expf on all 2^31 non-positive inputs (nqk_selftest_fastmath,
 // counts[3]).
 typedef float v2f_t __attribute__((ext_vector_type(2)));
+// element-pair arithmetic, packed (v_pk_*) or as two scalar instructions (PK = false: the same
+// IEEE operation per element; without the SLP vectorizer the pair stays unpacked)
+template <bool PK>
+__device__ __forceinline__ v2f_t vmul2(v2f_t a, v2f_t b) {
+  if constexpr (PK) return a * b;
+  else return v2f_t{a[0] * b[0], a[1] * b[1]};
+}
+template <bool PK>
+__device__ __forceinline__ v2f_t vadd2(v2f_t a, v2f_t b) {
+  if constexpr (PK) return a + b;
+  else return v2f_t{a[0] + b[0], a[1] + b[1]};
+}
+template <bool PK>
+__device__ __forceinline__ v2f_t vsub2(v2f_t a, v2f_t b) {
+  if constexpr (PK) return a - b;
+  else return v2f_t{a[0] - b[0], a[1] - b[1]};
+}
+template <bool PK>
+__device__ __forceinline__ v2f_t vfma2(v2f_t a, v2f_t b, v2f_t c) {
+  if constexpr (PK) return __builtin_elementwise_fma(a, b, c);
+  else return v2f_t{__builtin_fmaf(a[0], b[0], c[0]), __builtin_fmaf(a[1], b[1], c[1])};
+}
 __device__ __forceinline__ v2f_t np_expf_nonpos2(v2f_t x) {
   const v2f_t xc = v2f_t{__builtin_fmaxf(x[0], -128.0f), __builtin_fmaxf(x[1], -128.0f)};
   const float l2e = 1.442695040888963407359924681001892137f;
@@ -118,25 +140,26 @@ __device__ __forceinline__ v2f_t np_expf_nonpos2(v2f_t x) {
 // zero).  No clamp, no v_cvt / v_ldexp.  Equal to np_expf on every float of the domain
 // (nqk_selftest_fastmath, counts[4]).
 constexpr float NP_EXP_SAFE_LO = -86.5f;
+template <bool PK = true>
 __device__ __forceinline__ v2f_t np_expf_safe2(v2f_t x) {
   const float l2e = 1.442695040888963407359924681001892137f;
   const v2f_t mg = v2f_t{0x1.8p23f, 0x1.8p23f};
-  const v2f_t s = x * v2f_t{l2e, l2e} + mg;
-  const v2f_t q = s - mg;
-  v2f_t r = __builtin_elementwise_fma(q, v2f_t{-6.93145752e-1f, -6.93145752e-1f}, x);
-  r = __builtin_elementwise_fma(q, v2f_t{-1.42860677e-6f, -1.42860677e-6f}, r);
+  const v2f_t s = vadd2<PK>(vmul2<PK>(x, v2f_t{l2e, l2e}), mg);
+  const v2f_t q = vsub2<PK>(s, mg);
+  v2f_t r = vfma2<PK>(q, v2f_t{-6.93145752e-1f, -6.93145752e-1f}, x);
+  r = vfma2<PK>(q, v2f_t{-1.42860677e-6f, -1.42860677e-6f}, r);
   auto c2 = [](float c) { return v2f_t{c, c}; };
-  v2f_t num = __builtin_elementwise_fma(c2(5.082762527590693718096e-04f), r, c2(6.757896990527504603057e-03f));
-  num = __builtin_elementwise_fma(num, r, c2(5.114512081637298353406e-02f));
-  num = __builtin_elementwise_fma(num, r, c2(2.473615434895520810817e-01f));
-  num = __builtin_elementwise_fma(num, r, c2(7.257664613233124478488e-01f));
-  num = __builtin_elementwise_fma(num, r, c2(9.999999999980870924916e-01f));
-  v2f_t den = __builtin_elementwise_fma(c2(2.159509375685829852307e-02f), r, c2(-2.742335390411667452936e-01f));
-  den = __builtin_elementwise_fma(den, r, c2(1.0f));
+  v2f_t num = vfma2<PK>(c2(5.082762527590693718096e-04f), r, c2(6.757896990527504603057e-03f));
+  num = vfma2<PK>(num, r, c2(5.114512081637298353406e-02f));
+  num = vfma2<PK>(num, r, c2(2.473615434895520810817e-01f));
+  num = vfma2<PK>(num, r, c2(7.257664613233124478488e-01f));
+  num = vfma2<PK>(num, r, c2(9.999999999980870924916e-01f));
+  v2f_t den = vfma2<PK>(c2(2.159509375685829852307e-02f), r, c2(-2.742335390411667452936e-01f));
+  den = vfma2<PK>(den, r, c2(1.0f));
   const v2f_t rc = v2f_t{__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
-  const v2f_t qq = num * rc;
-  const v2f_t e = __builtin_elementwise_fma(-den, qq, num);
-  const v2f_t res = __builtin_elementwise_fma(e, rc, qq);
+  const v2f_t qq = vmul2<PK>(num, rc);
+  const v2f_t e = vfma2<PK>(-den, qq, num);
+  const v2f_t res = vfma2<PK>(e, rc, qq);
   return v2f_t{__uint_as_float(__float_as_uint(res[0]) + (__float_as_uint(s[0]) << 23)),
                __uint_as_float(__float_as_uint(res[1]) + (__float_as_uint(s[1]) << 23))};
 }
@@ -150,10 +173,11 @@ __device__ __forceinline__ v2f_t np_expf_safe2(v2f_t x) {
 // dd = c - (s - MAGIC) is the filter's distance to the rounded value (exact).  Replaces
 // v_rndne + add zp + med3 + v_cvt_pk_u8 + xor 0x80 per element (nqk_fused.hip
 // quant_filter); used by the GELU GEMM and the attention epilogues.
+template <bool PK = true>
 __device__ __forceinline__ v2f_t round_magic2(v2f_t x, float qlo, float qhi, float magic, v2f_t& dd) {
   const v2f_t c = v2f_t{__builtin_amdgcn_fmed3f(x[0], qlo, qhi), __builtin_amdgcn_fmed3f(x[1], qlo, qhi)};
-  const v2f_t s = c + v2f_t{magic, magic};
-  dd = c - (s - v2f_t{magic, magic});
+  const v2f_t s = vadd2<PK>(c, v2f_t{magic, magic});
+  dd = vsub2<PK>(c, vsub2<PK>(s, v2f_t{magic, magic}));
   return s;
 }
 // the low bytes of four rounded values (round_magic2) as one dword

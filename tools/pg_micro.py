@@ -135,7 +135,8 @@ for name in sel:
     for vname, env in envs.items():
         variants.append((f"pg:{vname}", main, env, True))
     if keep[-1] is not None:
-        variants.append(("glut", main, {}, "glut"))
+        for lname, lib in libs.items():
+            variants.append(("glut" if lname == "main" else f"glut:{lname}", lib, {}, "glut"))
     variants.append(("pg2", main, {"NQK_PG_KERNEL": "2"}, True))
     variants.append(("r02", main, {"NQK_PROJ_GELU": "1"} if epi == 4 else {}, False))
     res = {v[0]: [] for v in variants}

@@ -345,7 +345,44 @@ r4_t() {
   echo done >> gpurun_out/t.status
 }
 
+r4_u() {
+  # round-4 call U (run twice: the second time after the "scc" clobber fix in nqk_glut.h, with the
+  # main build's table / GEMM tests first): the GELU-table epilogue's f32 pairs unpacked through the vmul2 / vadd2 / vfma2
+  # helpers (NQK_PG_GLUT_UNPK=1, tools/diag/libnqk_glutu.so): the table tests with that library in
+  # place (box copy only), the FFN-up micro, whole-bench A/B (verified rows)
+  rm -f gpurun_out/u.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/u.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_glut.py tests/test_gpu_pgemm.py -x -q -rf --timeout 300 --timeout-method thread > gpurun_out/u_tests_main.log 2>&1
+  step glut_tests_main $?
+  cp numpy-quant_amd/numpy_quant/libnqk.so /tmp/libnqk_keep.so
+  cp tools/diag/libnqk_glutu.so numpy-quant_amd/numpy_quant/libnqk.so
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_glut.py -x -q -rf --timeout 300 --timeout-method thread > gpurun_out/u_tests.log 2>&1
+  rc=$?
+  cp /tmp/libnqk_keep.so numpy-quant_amd/numpy_quant/libnqk.so
+  step glut_tests_glutu $rc
+  timeout -k 10 300 env PGM_LIBS=glutu=tools/diag/libnqk_glutu.so PGM_SHAPES=up PGM_ROUNDS=3 python -u tools/pg_micro.py > gpurun_out/u_pg_micro.txt 2>&1
+  step pg_micro $?
+  AB_LIBS="main glutu" AB_REPS=2 OUT=u bash tools/ab.sh
+  step ab $?
+  echo done >> gpurun_out/u.status
+}
+
+r4_final() {
+  # round-4 closing evidence call: the whole GPU test suite, the default bench line, then
+  # tools/gpu_full.sh's rocprofv3 kernel trace of a short one-stream bench and the FETCH_SIZE /
+  # WRITE_SIZE passes (profiles/r04_final_*)
+  rm -f gpurun_out/full.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/full.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+  step pytest $?
+  timeout -k 10 400 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+  step bench $?
+  SKIP_TESTS=1 SKIP_BENCH=1 bash tools/gpu_full.sh
+  step gpu_full $?
+  echo done >> gpurun_out/full.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|final) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|final}" >&2; exit 2 ;;
 esac
