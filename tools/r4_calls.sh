@@ -382,7 +382,22 @@ r4_final() {
   echo done >> gpurun_out/full.status
 }
 
+r4_v() {
+  # round-4 call V: the two half-batch streams out of phase (NQK_STREAM_OFFSET: the side stream
+  # starts after part 0's embedding, or after a stage of part 0's first layer): parity of the
+  # B = 256 forward under each offset, then whole-bench A/B (every row verified)
+  rm -f gpurun_out/v.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/v.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  for o in embed attn; do
+    NQK_STREAM_OFFSET=$o timeout -k 10 400 python -u -m pytest tests/test_gpu_b256.py -x -q --timeout 300 --timeout-method thread > gpurun_out/v_tests_$o.log 2>&1
+    step tests_$o $?
+  done
+  AB_ENVS="embed:NQK_STREAM_OFFSET=embed qkv:NQK_STREAM_OFFSET=qkv attn:NQK_STREAM_OFFSET=attn ln2:NQK_STREAM_OFFSET=ln2 up:NQK_STREAM_OFFSET=up" AB_REPS=2 OUT=v bash tools/ab.sh
+  step ab $?
+  echo done >> gpurun_out/v.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|final) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|final}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|final) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|final}" >&2; exit 2 ;;
 esac
