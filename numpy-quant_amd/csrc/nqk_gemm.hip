@@ -411,6 +411,9 @@ k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __
 // rows (3 x 16 B) of its patch for the current kernel row ki (3 k-tiles) in registers and
 // writes its 8 k values of each k-tile as two ds_write_b128.
 constexpr int EQ_ROW = 20;  // floats per LDS operand row (16 + 4 padding)
+#ifndef NQK_EMBED_PXD
+#define NQK_EMBED_PXD 1
+#endif
 template <int WN>
 __global__ void __launch_bounds__(256, 2)
 k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __restrict__ C, int64_t M, int64_t N,
@@ -491,7 +494,12 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
     const bool more = kt + 1 < NKT;
     if (more) {
       load_b(kt + 1);
-      if constexpr (sub == 2) load_px((kt + 1) / 3, pxn);
+      // the next kernel row's image bytes (HBM): NQK_EMBED_PXD 1 = issued at the row's first
+      // k-tile, three k-tiles before their use; 0 = in the k-tile before it
+      if constexpr (NQK_EMBED_PXD == 0 && sub == 2) load_px((kt + 1) / 3, pxn);
+    }
+    if constexpr (NQK_EMBED_PXD == 1 && sub == 0) {
+      if (kt + 3 < NKT) load_px(kt / 3 + 1, pxn);
     }
     v4f fa[2][2], fb[WN][2];
 #pragma unroll

@@ -397,7 +397,20 @@ r4_v() {
   echo done >> gpurun_out/v.status
 }
 
+r4_w() {
+  # round-4 call W: the patch embedding's next-kernel-row image loads issued three k-tiles ahead
+  # (NQK_EMBED_PXD=1) instead of one (pxd0): parity (the fused embedding against the im2col
+  # path, the B = 256 forward), whole-bench A/B
+  rm -f gpurun_out/w.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/w.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_fused_kernels.py tests/test_gpu_b256.py tests/test_gpu_l1.py -x -q --timeout 300 --timeout-method thread > gpurun_out/w_tests.log 2>&1
+  step tests $?
+  AB_LIBS="main pxd0" AB_REPS=3 OUT=w bash tools/ab.sh
+  step ab $?
+  echo done >> gpurun_out/w.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|final) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|final}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|w|final) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|w|final}" >&2; exit 2 ;;
 esac
