@@ -410,7 +410,19 @@ r4_w() {
   echo done >> gpurun_out/w.status
 }
 
+r4_x() {
+  # round-4 call X: sanity of the rebuilt library (same sources): smoke(), the table / GEMM /
+  # B = 256 parity tests
+  rm -f gpurun_out/x.status
+  step() { echo "== $1 rc=$2" >> gpurun_out/x.status; if [ $2 -ne 0 ]; then exit $2; fi; }
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/x_smoke.log 2>&1
+  step smoke $?
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_glut.py tests/test_gpu_pgemm.py tests/test_gpu_b256.py -x -q --timeout 300 --timeout-method thread > gpurun_out/x_tests.log 2>&1
+  step tests $?
+  echo done >> gpurun_out/x.status
+}
+
 case "${1:-}" in
-  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|w|final) "r4_$1" ;;
-  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|w|final}" >&2; exit 2 ;;
+  probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|w|x|final) "r4_$1" ;;
+  *) echo "usage: tools/r4_calls.sh {probe|eval|b|c|d|e|f|g|h|j|k|l|m|n|o|p|q|r|s|t|u|v|w|x|final}" >&2; exit 2 ;;
 esac
