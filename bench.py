@@ -80,22 +80,45 @@ def rank_environments(n: int, port: int, base: dict | None = None) -> list[dict]
     return envs
 
 
-def spawn_ranks(n: int, argv: list[str], timeout: float | None = None) -> int:
+def spawn_ranks(n: int, argv: list[str], timeout: float | None = None, script: str | None = None,
+                poll_s: float = 0.2) -> int:
     """Run this script once per rank as child processes (this process never touches
-    the GPU) and return the first non-zero exit status, or 0."""
+    the GPU) and return the first non-zero exit status, or 0.  Fail fast: every child is
+    polled, and the first one that exits non-zero (a dead rank would leave the others
+    blocked in a collective or a control-plane wait) has the others killed at once and its
+    status returned; past `timeout` seconds every rank is killed and 124 returned."""
     port = _free_port()
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env)
-             for env in rank_environments(n, port)]
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + argv, env=env) for env in rank_environments(n, port)]
+    t0 = time.monotonic()
     rc = 0
     try:
-        for p in procs:
-            r = p.wait(timeout=timeout)
-            rc = rc or r
+        while True:
+            live = 0
+            for p in procs:
+                r = p.poll()
+                if r is None:
+                    live += 1
+                elif r != 0:
+                    rc = r if r > 0 else 128 - r  # a signal -s: 128 + s, as a shell reports it
+                    print(f"bench.py: rank {procs.index(p)} exited with status {r}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    return rc
+            if live == 0:
+                return 0
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                print(f"bench.py: ranks still running after {timeout:.0f} s; stopping them", file=sys.stderr, flush=True)
+                return 124
+            time.sleep(poll_s)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    return rc
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                pass
 
 
 # ----------------------------------------------------------------------------- models
@@ -127,7 +150,7 @@ def build_vit(batch: int, bit_width: int, group, calib_batch: int = 8, tiny: boo
 
 
 VIT_TINY = (192, 3, 768)  # ViT-Ti/16: width, heads, MLP width (head size 64 and depth 12 as ViT-Base)
-PROJ_TAGS = ("qgemm_qkv", "qgemm_resid", "qgemm_gelu")  # MatMuls with constant weights (k_pg)
+PROJ_TAGS = ("qgemm_qkv", "qgemm_out", "qgemm_gelu", "qgemm_down")  # MatMuls with constant weights (k_pg)
 
 
 def kernel_breakdown(qmodel, x_dev):
@@ -168,27 +191,39 @@ def kernel_breakdown(qmodel, x_dev):
             gbs = d["bytes"] / (d["ms"] * 1e-3) / 1e9
             e.update(achieved=round(gbs, 1), unit="GB/s", frac=round(gbs / HBM_PEAK_GBS, 4))
         out[tag] = e
+    for tag in PROJ_TAGS:  # the projection GEMMs' algorithmic HBM rate as well
+        if tag in by and tag in out:
+            d = by[tag]
+            out[tag]["hbm_gbs"] = round(d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1)
+            out[tag]["hbm_frac"] = round(d["bytes"] / (d["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     proj = [by[t] for t in PROJ_TAGS if t in by]
-    pm = sum(d["ms"] for d in proj)
-    po = sum(d["ops"] for d in proj)
-    pl = sum(d["launches"] for d in proj)
-    return out, {"ms": pm, "ops": po, "launches": pl}
+    summ = {"ms": sum(d["ms"] for d in proj), "ops": sum(d["ops"] for d in proj),
+            "bytes": sum(d["bytes"] for d in proj), "launches": sum(d["launches"] for d in proj)}
+    att = by.get("attention", {"ms": 0.0, "ops": 0})
+    summ["attn_ms"], summ["attn_ops"] = att["ms"], att["ops"]
+    summ["int8_ops"] = sum(d["ops"] for t, d in by.items() if d["unit"] != "flop32")
+    return out, summ
 
 
-def traffic_from_profiles(kernel_families):
-    """HBM bytes per launch of the projection GEMMs (mean over the launches of the given
-    kernel families) from the committed PMC summary (profiles/pmc_traffic.json, collected
-    with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH_SIZE doubled for
-    gfx950 per MI355X_MICROARCH.md), or None."""
+def traffic_from_profiles(tiny: bool = False):
+    """HBM bytes per launch of the forward's projection GEMMs, per shape, from the committed
+    PMC summary (profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in
+    separate passes over a one-stream B = 256 bench forward, FETCH_SIZE doubled for gfx950 per
+    MI355X_MICROARCH.md; tools/pmc_traffic.py keys it by kernel template and grid).  Only the
+    int8 k_pg launches of the benchmarked shapes at the B = 256 grid count: ViT-Base K in
+    {768, 3072} (template NK 12 / 48) or ViT-Ti K in {192, 768} (NK 3 / 12 at N < 768), int8
+    weights (B4 false).  Returns (mean bytes per launch, {shape: bytes}) or (None, None)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         data = json.load(open(path))
     except (OSError, ValueError):
-        return None
-    ents = [data.get("kernels", {}).get(k) for k in kernel_families]
-    ents = [e for e in ents if e]
-    n = sum(e["launches"] for e in ents)
-    return round(sum(e["launches"] * e["hbm_bytes_per_launch"] for e in ents) / n) if n else None
+        return None, None
+    per = data.get("per_shape_tiny" if tiny else "per_shape")
+    if not per:
+        return None, None
+    vals = {k: v["hbm_bytes_per_launch"] for k, v in per.items()}
+    # every shape runs once per layer: the per-launch mean weights them equally
+    return round(sum(vals.values()) / len(vals)), vals
 
 
 def host_cpu() -> dict:
@@ -204,28 +239,43 @@ def host_cpu() -> dict:
     return {"cpu_model": model, "nproc": os.cpu_count()}
 
 
-def cpu_baseline_vit(bit_width: int, tiny: bool = False) -> dict:
-    """The oracle (CPU restatement of the reference, int64 np.matmul) on a bounded
-    sample: one ViT-Base encoder layer at batch 1 (12 of these are 99 % of a
-    forward), scaled x12 to a per-image rate."""
+def cpu_baseline_vit(bit_width: int, tiny: bool = False, mode: str = "full") -> dict:
+    """The oracle (CPU restatement of the reference's QModel.__call__, int64 np.matmul) on a
+    bounded sample of the same workload.  mode "full" (default, BASELINE.md's plan): the whole
+    classifier forward (patch embedding, 12 encoder layers, classifier) on ONE image, measured
+    (~30 s for ViT-Base on one core); mode "layer": one encoder layer at batch 1, x12
+    (extrapolated: drops the embedding and the classifier, ~3 s)."""
     import numpy as np
     from numpy_quant import onnx_proto
     from oracle import nq_oracle as O
-    proto = onnx_proto.load(LAYER_FILE, synthetic_weights=True)
-    if tiny:
-        onnx_proto.redimension(proto, *VIT_TINY)
-    g = O.Graph(proto)
+    arch = "Ti" if tiny else "Base"
     rng = np.random.default_rng(7)
-    x = rng.standard_normal((1, 197, VIT_TINY[0] if tiny else 768)).astype(np.float32)
+    if mode == "layer":
+        proto = onnx_proto.load(LAYER_FILE, synthetic_weights=True)
+        if tiny:
+            onnx_proto.redimension(proto, *VIT_TINY)
+        x = rng.standard_normal((1, 197, VIT_TINY[0] if tiny else 768)).astype(np.float32)
+    else:
+        proto = onnx_proto.load(MODEL_FILE, synthetic_weights=True)
+        if tiny:
+            onnx_proto.redimension(proto, *VIT_TINY)
+        x = rng.standard_normal((1, 3, 224, 224)).astype(np.float32)
+    g = O.Graph(proto)
     with np.errstate(all="ignore"):
         qp, qc = O.calibrate(g, [x], bit_width)
         t0 = time.perf_counter()
         O.quantized_forward(g, qp, qc, [x], bit_width)
         dt = time.perf_counter() - t0
-    per_image = 12 * dt
+    if mode == "layer":
+        per_image = 12 * dt
+        sample = (f"EXTRAPOLATED: oracle QModel forward of 1 ViT-{arch} encoder layer, batch 1 ({dt:.1f} s), x12 layers "
+                  "(embedding and classifier not timed)")
+    else:
+        per_image = dt
+        sample = (f"measured: oracle QModel forward of the whole ViT-{arch}/16 classifier (patch embedding, 12 encoder "
+                  f"layers, classifier) on 1 image, {dt:.1f} s")
     res = {"value": 1.0 / per_image, "unit": "samples/s", "cores": 1, "kind": "port",
-           "sample": f"oracle QModel forward of 1 ViT-{'Ti' if tiny else 'Base'} encoder layer, batch 1 ({dt:.1f} s), x12 layers; "
-                     "int64 np.matmul is single-threaded (99% of the time)"}
+           "sample": sample + "; int64 np.matmul is single-threaded (99% of the time)"}
     res.update(host_cpu())
     return res
 
@@ -308,6 +358,10 @@ def run_vit(args, group):
     if rank != 0:
         return None
     achieved = proj["ops"] / (proj["ms"] * 1e-3) / 1e12
+    # every int8 MatMul of the forward: the 48 projections + the 24 attention products
+    mm_tops = (proj["ops"] + proj["attn_ops"]) / ((proj["ms"] + proj["attn_ms"]) * 1e-3) / 1e12
+    step_tops = proj["int8_ops"] / (ms_per_step * 1e-3) / 1e12 / world
+    traffic, traffic_by = traffic_from_profiles(tiny) if bw == 8 else (None, None)
     res = result_head(args, world, ms_per_step, value, f"int{bw}")
     arch = ("ViT-Ti/16-224: the graph re-dimensioned to width 192, 3 heads, MLP 768 (onnx_proto.redimension)"
             if tiny else "ViT-Base/16-224")
@@ -321,17 +375,32 @@ def run_vit(args, group):
     res["matmul_tops"] = round(achieved, 2)
     res["roofline"] = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(INT8_PEAK_TOPS, 1),
                        "unit": "TOPS", "frac": round(achieved / INT8_PEAK_TOPS, 4),
-                       "traffic": traffic_from_profiles(("k_pg",)) if bw == 8 else None,
+                       "traffic": traffic, "traffic_by_shape": traffic_by,
+                       "traffic_note": "PMC HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE) of this config's int8 "
+                                       "k_pg launches at the B=256 grid, mean over the 4 shapes "
+                                       "(profiles/pmc_traffic.json)",
                        "kernel": "the 48 int8 MFMA projection GEMMs of one forward, fused epilogues: k_pg "
-                                 "(persistent 128x256 tiles, v_mfma_i32_16x16x64_i8, two workgroups per CU) for "
-                                 "QKV + head split, FFN up + GELU, attention output + residual, FFN down + "
-                                 "residual; 2*M*N*K int8 ops per launch",
+                                 "(persistent, v_mfma_i32_16x16x64_i8) for QKV + head split, FFN up + GELU, "
+                                 "attention output + residual, FFN down + residual; 2*M*N*K int8 ops per launch",
                        "launches": proj["launches"], "avg_launch_us": round(1e3 * proj["ms"] / max(1, proj["launches"]), 2),
-                       "gemm_ms_per_forward": round(proj["ms"], 3)}
+                       "gemm_ms_per_forward": round(proj["ms"], 3),
+                       "gemm_hbm_gbs": round(proj["bytes"] / (proj["ms"] * 1e-3) / 1e9, 1),
+                       "gemm_hbm_frac": round(proj["bytes"] / (proj["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "matmul_path_frac": round(mm_tops / INT8_PEAK_TOPS, 4),
+                       "matmul_path_note": "all 72 int8 MatMuls of a forward (48 projections + 24 attention QK^T / "
+                                           "PV inside k_attention) over their one-stream launch time",
+                       "int8_ops_per_step_frac": round(step_tops / INT8_PEAK_TOPS, 4),
+                       "int8_ops_per_step_note": "every int8 MatMul op of a forward / ms_per_step (the whole "
+                                                 "two-stream step, every other kernel included)"}
+    if tiny:  # ViT-Ti's GEMMs (K = 192 / 768, N = 192 .. 768) are HBM-bound: priced against HBM
+        r = res["roofline"]
+        r.update(bound="hbm", achieved=r["gemm_hbm_gbs"], peak=HBM_PEAK_GBS, unit="GB/s", frac=r["gemm_hbm_frac"],
+                 mfma_frac=round(achieved / INT8_PEAK_TOPS, 4),
+                 kernel=r["kernel"] + "; algorithmic bytes per launch = A + weights + outputs (residual: f32 in + out)")
     res["kernels"] = kern
     res.update(ver)
     if not args.no_cpu_baseline and world == 1:
-        res["cpu_baseline"] = cpu_baseline_vit(bw, tiny)
+        res["cpu_baseline"] = cpu_baseline_vit(bw, tiny, args.cpu_baseline)
     return res
 
 
@@ -409,6 +478,8 @@ def main(argv=None):
     ap.add_argument("--bit-width", type=int, default=8)
     ap.add_argument("--config", choices=("vit", "vit_int4", "vit_tiny", "mlp4096"), default="vit")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline", choices=("full", "layer"), default="full",
+                    help="full: the oracle's whole ViT forward on one image (measured); layer: one layer x12")
     ap.add_argument("--no-secondary", action="store_true", help="skip the int4 / ViT-tiny / MLP-4096 lines")
     ap.add_argument("--graph", type=int, default=0, help="1: replay the ViT forward as one captured hipGraph")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # launcher test: no GPU
@@ -424,6 +495,8 @@ def main(argv=None):
               file=sys.stderr)
         sys.exit(2)
 
+    if args.dry_run and os.environ.get("NQK_DRY_RUN_EXIT_RANK") == os.environ.get("RANK", "0"):
+        sys.exit(3)  # launcher test: this rank dies before the rendezvous (tests/test_launcher.py)
     from numpy_quant.replicas import ReplicaGroup
     group = ReplicaGroup()
     if args.dry_run:
@@ -467,6 +540,9 @@ def run_secondary(args, group) -> dict:
             out[cfg] = {k: r[k] for k in keep if k in r}
             if "roofline" in r:
                 out[cfg]["roofline_frac"] = r["roofline"]["frac"]
+            if cfg == "vit_tiny":  # the metric's named workload: the same breakdown as the headline
+                out[cfg]["roofline"] = r["roofline"]
+                out[cfg]["kernels"] = r["kernels"]
         except Exception as e:  # a failing secondary must not lose the headline line
             out[cfg] = {"error": repr(e)[:300]}
         log(f"[bench] secondary {cfg}: {out[cfg].get('value')} samples/s in {time.time() - t0:.1f}s")

@@ -286,8 +286,9 @@ int nqk_pack_pg4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t l
 /* The FFN-up epilogue's GELU chain as a table (round 4): model.py Div -> Erf -> Add -> Mul ->
  * Mul on f32 (numpy_helper.py:95-112 erf) followed by numpy_quantization.py:24-34 quantize
  * with (s_out, zp_out, bit_width), as a step function of the dequantized, biased f32 value h:
- * at most 512 buckets of 8 bytes in lut (a 4 KiB, 16-byte aligned device buffer), the bucket
- * coordinate in k_out[5], the entry count in *n_out.  Every entry comes from the exact chain,
+ * at most 1024 buckets of 8 bytes in lut (an 8 KiB, 16-byte aligned device buffer), the bucket
+ * coordinate in k_out[5], the entry count in *n_out (the 128 x 256-tile k_pg takes tables of up
+ * to 512 entries, the 256 x 256 one up to 1024; the builder prefers <= 512).  Every entry comes from the exact chain,
  * and the table is then compared with the exact chain on all 2^32 - 2^24 finite f32 inputs:
  * *n_out = 0 (return 0) when the table cannot represent the chain exactly, when the chain is
  * not the GELU of model.py (div = f32(sqrt 2), add1 = 1, mul2 = 0.5) or bit_width is not in
@@ -304,8 +305,8 @@ int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64_t batch, i
 /* Which kernel the last nqk_qgemm_fused call launched (tests / diagnostics): 0 small tiles
  * (k_qgemm_epi), 1 128x256 tiles (k_qgemm_big), 2 ping-pong 256x256 (k_qgemm_pp), 3 the
  * persistent projection GEMM with the epilogue overlapped (k_proj), 4 the persistent 16x16x64
- * GEMM with two workgroups per CU (k_pg), 5 the persistent 16x16x64 GEMM with each tile's
- * epilogue inside the next tile's k loop (k_pg2), 6 k_pg with the GELU table epilogue
+ * GEMM with two workgroups per CU (k_pg), 5 k_pg on 256 x 256 tiles (one 512-thread workgroup
+ * per CU, B shared by its two row halves), 6 / 7 the same two with the GELU table epilogue
  * (nqk_gelu_lut_build); -1 none yet. */
 int nqk_qgemm_last_kernel(void);
 /* LayerNormalization (model.py:134-152) fused with the consumer MatMul's quantize */

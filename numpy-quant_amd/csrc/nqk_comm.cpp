@@ -3,7 +3,9 @@
 // per-rank outputs.  The reference is single-process NumPy and
 // has no collective of its own; there is no exchange in the per-forward data path.
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "nqk_common.h"
 
@@ -13,6 +15,37 @@ int g_nranks = 1, g_rank = 0;
 int nccl_check(ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return 0;
   return nqk::fail(std::string(what) + ": " + ncclGetErrorString(r));
+}
+double now_s() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+// The communicator is non-blocking (config.blocking = 0), so that a rank whose peer died
+// before joining does not wait forever inside ncclCommInitRank: every call returns
+// ncclInProgress until its host-side work is done, polled here against a deadline
+// (NQK_COMM_TIMEOUT_S, default 120 s); past it the communicator is aborted and the call fails.
+double comm_deadline_s() {
+  const char* v = getenv("NQK_COMM_TIMEOUT_S");
+  const double d = v ? atof(v) : 120.0;
+  return d > 0 ? d : 120.0;
+}
+int nccl_wait(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess && r != ncclInProgress) return nccl_check(r, what);
+  const double t0 = now_s(), lim = comm_deadline_s();
+  while (r == ncclInProgress) {
+    if (ncclCommGetAsyncError(g_comm, &r) != ncclSuccess) break;
+    if (r != ncclInProgress) break;
+    if (now_s() - t0 > lim) {
+      ncclCommAbort(g_comm);
+      g_comm = nullptr;
+      return nqk::fail(std::string(what) + ": not complete after " + std::to_string((int)lim) +
+                       " s (a peer rank is gone?); communicator aborted");
+    }
+    timespec ts{0, 200000};  // 0.2 ms
+    nanosleep(&ts, nullptr);
+  }
+  return nccl_check(r, what);
 }
 }  // namespace
 
@@ -28,7 +61,14 @@ int nqk_comm_unique_id(void* id128) {
 int nqk_comm_init(const void* id128, int nranks, int rank) {
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
-  if (nccl_check(ncclCommInitRank(&g_comm, nranks, id, rank), "ncclCommInitRank")) return -1;
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  const ncclResult_t r = ncclCommInitRankConfig(&g_comm, nranks, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    g_comm = nullptr;
+    return nccl_check(r, "ncclCommInitRankConfig");
+  }
+  if (nccl_wait(r, "ncclCommInitRankConfig")) return -1;
   g_nranks = nranks;
   g_rank = rank;
   return 0;
@@ -36,12 +76,12 @@ int nqk_comm_init(const void* id128, int nranks, int rank) {
 
 int nqk_comm_bcast(void* buf, size_t bytes, int root) {
   if (!g_comm) return nqk::fail("communicator not initialised");
-  return nccl_check(ncclBroadcast(buf, buf, bytes, ncclInt8, root, g_comm, nqk::stream()), "ncclBroadcast");
+  return nccl_wait(ncclBroadcast(buf, buf, bytes, ncclInt8, root, g_comm, nqk::stream()), "ncclBroadcast");
 }
 
 int nqk_comm_gather(const void* send, void* recv, size_t bytes_per_rank, int root) {
   if (!g_comm) return nqk::fail("communicator not initialised");
-  return nccl_check(ncclGather(send, recv, bytes_per_rank, ncclInt8, root, g_comm, nqk::stream()), "ncclGather");
+  return nccl_wait(ncclGather(send, recv, bytes_per_rank, ncclInt8, root, g_comm, nqk::stream()), "ncclGather");
 }
 
 int nqk_comm_barrier(void) {
@@ -49,14 +89,19 @@ int nqk_comm_barrier(void) {
   // a 4-byte all-reduce on the library stream, then a stream sync
   static void* scratch = nullptr;
   if (!scratch && nqk::check(hipMalloc(&scratch, 16), "hipMalloc")) return -1;
-  if (nccl_check(ncclAllReduce(scratch, scratch, 1, ncclInt32, ncclSum, g_comm, nqk::stream()), "ncclAllReduce"))
+  if (nccl_wait(ncclAllReduce(scratch, scratch, 1, ncclInt32, ncclSum, g_comm, nqk::stream()), "ncclAllReduce"))
     return -1;
   return nqk::check(hipStreamSynchronize(nqk::stream()), "hipStreamSynchronize");
 }
 
 int nqk_comm_destroy(void) {
   if (!g_comm) return 0;
-  ncclResult_t r = ncclCommDestroy(g_comm);
+  // non-blocking communicator: finalize (polled), then destroy
+  ncclResult_t r = ncclCommFinalize(g_comm);
+  if (r == ncclSuccess || r == ncclInProgress) {
+    if (nccl_wait(r, "ncclCommFinalize")) return -1;
+  }
+  r = ncclCommDestroy(g_comm);
   g_comm = nullptr;
   return nccl_check(r, "ncclCommDestroy");
 }

@@ -1812,7 +1812,8 @@ static void launch_big(bool pp, const int8_t* a, const int8_t* bt, int64_t M, in
   }
 }
 
-static int g_last_gemm = -1;  // nqk_qgemm_last_kernel: 0 small tiles, 1 big tile, 2 ping-pong, 3 persistent, 4 k_pg
+static int g_last_gemm = -1;  // nqk_qgemm_last_kernel: 0 small tiles, 1 big tile, 2 ping-pong, 3 persistent, 4 k_pg,
+                              // 5 k_pg 256 x 256 (WM = 2), 6 / 7 the same two with the GELU table
 namespace nqk {
 int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, int64_t K, int64_t lda,
               const nqk_epilogue* p, bool f32x);  // nqk_pgemm.hip

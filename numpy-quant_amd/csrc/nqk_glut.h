@@ -25,7 +25,9 @@
 namespace nqk {
 namespace {
 
-constexpr int GLUT_MAX = 512;  // entries of 8 bytes: 4 KiB of LDS per workgroup
+constexpr int GLUT_MAX = 1024;  // entries of 8 bytes: the builder's capacity (8 KiB)
+constexpr int GLUT_CAP1 = 512;  // what the 128 x 256-tile k_pg holds in LDS (4 KiB; two workgroups
+                                // per CU); the 256 x 256 one (WM = 2) holds GLUT_MAX
 constexpr float GLUT_MAGIC = 0x1.8p23f;
 constexpr uint32_t GLUT_MAGIC_BITS = 0x4B400000u;
 

@@ -143,25 +143,29 @@ extern "C" int nqk_gelu_lut_build(float s_out, int64_t zp_out, int32_t bit_width
   double hr = yr <= gmin ? hk + 1e-3 : (yr >= gelu_d(1e6) ? 1e6 : gelu_solve(hk, 1e6, yr));
   double hl = yl <= gmin ? hk - 1e-3 : gelu_solve(-40.0, hk, yl);
   // bucket widths below the closest spacing of two output steps on each branch (max slope
-  // 1.129 on the increasing branch, 0.129 on the decreasing one)
-  double wl = 3.0 * s;
-  int n = 0, nl = 0;
-  double wr = 0.0;
-  for (double f : {0.75, 0.85}) {
-    wr = f * s;
-    nl = (int)std::ceil((hk - (hl - 2.0 * wl)) / wl);
-    const int nr = (int)std::ceil(((hr + 2.0 * wr) - hk) / wr);
-    n = nl + nr + 2;
-    if (n <= GLUT_MAX) break;
-  }
-  if (n > GLUT_MAX || n < 3) return 0;
-  const double M = GLUT_MAGIC;
-  GLutK k;
-  k.iwR = (float)(1.0 / wr);
-  k.cR = (float)(M + nl + 1 - hk * (double)k.iwR);
-  k.iwL = (float)(1.0 / wl);
-  k.cL = (float)(M + nl + 1 - hk * (double)k.iwL);
-  k.uhi = (float)(M + n - 1);
+  // 1.129 on the increasing branch: s / 1.129 = 0.886 s; 0.129 on the decreasing one: 7.75 s).
+  // Candidates, finest first: the first that fits the 128 x 256-tile kernel's 512 entries, else
+  // the first that fits GLUT_MAX; a candidate whose exhaustive check fails gives way to the next
+  // (round 5: ViT-Ti's FFN-up outputs, s ~ 0.0052 .. 0.0058, need ~650 entries at (0.75 s, 3 s),
+  // ~520 at (0.85 s, 6 s), ~500 at (0.88 s, 7 s))
+  struct Cand { double fr, fl; };
+  const Cand cands[] = {{0.75, 3.0}, {0.85, 3.0}, {0.85, 6.0}, {0.88, 7.0}};
+  auto count = [&](const Cand& c, int& nl_) {
+    const double wr_ = c.fr * s, wl_ = c.fl * s;
+    nl_ = (int)std::ceil((hk - (hl - 2.0 * wl_)) / wl_);
+    const int nr_ = (int)std::ceil(((hr + 2.0 * wr_) - hk) / wr_);
+    return nl_ + nr_ + 2;
+  };
+  std::vector<Cand> order;
+  for (int cap : {GLUT_CAP1, GLUT_MAX})
+    for (const Cand& c : cands) {
+      int nl_ = 0;
+      const int n_ = count(c, nl_);
+      bool seen = false;
+      for (const Cand& o : order) seen = seen || (o.fr == c.fr && o.fl == c.fl);
+      if (n_ >= 3 && n_ <= cap && !seen) order.push_back(c);
+    }
+  if (order.empty()) return 0;
   GLutQ q;
   q.rdiv = 1.0 / (double)div;
   q.rs = 1.0 / (double)s_out;
@@ -179,68 +183,81 @@ extern "C" int nqk_gelu_lut_build(float s_out, int64_t zp_out, int32_t bit_width
     (void)hipFree(bad);
     return rc;
   };
-  int rc = check(hipMemsetAsync(err, 0, 4, stream()), "nqk_gelu_lut_build(memset)");
-  if (rc) return done(rc);
-  hipLaunchKernelGGL(k_glut_build, dim3((n + 63) / 64), dim3(64), 0, stream(), (uint2*)lut, n, k, q, err);
-  if ((rc = launch_status("nqk_gelu_lut_build(build)"))) return done(rc);
-  unsigned herr = 0;
-  if ((rc = check(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream()), "nqk_gelu_lut_build(copy)"))) return done(rc);
-  // check; where a bucket's mismatches lie within 256 floats next to its window (or, in a
-  // bucket without a change, anywhere), widen / place the window over them and check again
-  std::vector<uint2> tab(n);
-  auto verify = [&](GLutBad& hb) {
-    int r = check(hipMemsetAsync(bad, 0, sizeof(GLutBad), stream()), "nqk_gelu_lut_build(memset)");
-    if (!r) r = check(hipMemsetAsync(bad->kmin, 0xff, sizeof(unsigned) * GLUT_MAX, stream()), "nqk_gelu_lut_build(memset)");
-    if (r) return r;
-    hipLaunchKernelGGL(k_glut_verify, dim3(2048), dim3(256), 0, stream(), (const uint2*)lut, n, k, q, bad);
-    if ((r = launch_status("nqk_gelu_lut_build(verify)"))) return r;
-    if ((r = check(hipMemcpyAsync(&hb, bad, sizeof(GLutBad), hipMemcpyDeviceToHost, stream()), "nqk_gelu_lut_build(copy)")))
-      return r;
-    return check(hipStreamSynchronize(stream()), "nqk_gelu_lut_build(sync)");
-  };
-  GLutBad hb;
-  for (int pass = 0; pass < 2 && !herr; ++pass) {
-    if ((rc = verify(hb))) return done(rc);
-    if (hb.total == 0) {
-      k_out[0] = k.iwR;
-      k_out[1] = k.cR;
-      k_out[2] = k.iwL;
-      k_out[3] = k.cL;
-      k_out[4] = k.uhi;
-      *n_out = n;
-      return done(0);
-    }
-    if (pass == 1) break;
-    if ((rc = check(hipMemcpy(tab.data(), lut, 8 * (size_t)n, hipMemcpyDeviceToHost), "nqk_gelu_lut_build(read)")))
+  for (const Cand& c : order) {
+    int nl = 0;
+    const int n = count(c, nl);
+    const double wr = c.fr * s, wl = c.fl * s;
+    const double M = GLUT_MAGIC;
+    GLutK k;
+    k.iwR = (float)(1.0 / wr);
+    k.cR = (float)(M + nl + 1 - hk * (double)k.iwR);
+    k.iwL = (float)(1.0 / wl);
+    k.cL = (float)(M + nl + 1 - hk * (double)k.iwL);
+    k.uhi = (float)(M + n - 1);
+    int rc = check(hipMemsetAsync(err, 0, 4, stream()), "nqk_gelu_lut_build(memset)");
+    if (rc) return done(rc);
+    hipLaunchKernelGGL(k_glut_build, dim3((n + 63) / 64), dim3(64), 0, stream(), (uint2*)lut, n, k, q, err);
+    if ((rc = launch_status("nqk_gelu_lut_build(build)"))) return done(rc);
+    unsigned herr = 0;
+    if ((rc = check(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream()), "nqk_gelu_lut_build(copy)")))
       return done(rc);
-    bool ok = true;
-    for (int i = 0; i < n && ok; ++i) {
-      if (!hb.cnt[i]) continue;
-      auto fl = [](unsigned key) {  // key -> float bits
-        return (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
-      };
-      auto key_of = [](uint32_t bits) { return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u); };
-      unsigned lo = hb.kmin[i], hi = hb.kmax[i];
-      const uint32_t thr = tab[i].x, K = (tab[i].y >> 8) & 0xffu;
-      const bool has_change = (tab[i].y & 0xffu) != ((tab[i].y >> 16) & 0xffu);
-      if (has_change) {  // the existing window in keys
-        const bool neg = thr >> 31;
-        const unsigned wa = neg ? key_of(thr + K) : key_of(thr), wb = neg ? key_of(thr) : key_of(thr + K);
-        lo = lo < wa ? lo : wa;
-        hi = hi > wb ? hi : wb;
+    // check; where a bucket's mismatches lie within 256 floats next to its window (or, in a
+    // bucket without a change, anywhere), widen / place the window over them and check again
+    std::vector<uint2> tab(n);
+    auto verify = [&](GLutBad& hb) {
+      int r = check(hipMemsetAsync(bad, 0, sizeof(GLutBad), stream()), "nqk_gelu_lut_build(memset)");
+      if (!r) r = check(hipMemsetAsync(bad->kmin, 0xff, sizeof(unsigned) * GLUT_MAX, stream()), "nqk_gelu_lut_build(memset)");
+      if (r) return r;
+      hipLaunchKernelGGL(k_glut_verify, dim3(2048), dim3(256), 0, stream(), (const uint2*)lut, n, k, q, bad);
+      if ((r = launch_status("nqk_gelu_lut_build(verify)"))) return r;
+      if ((r = check(hipMemcpyAsync(&hb, bad, sizeof(GLutBad), hipMemcpyDeviceToHost, stream()), "nqk_gelu_lut_build(copy)")))
+        return r;
+      return check(hipStreamSynchronize(stream()), "nqk_gelu_lut_build(sync)");
+    };
+    GLutBad hb;
+    for (int pass = 0; pass < 2 && !herr; ++pass) {
+      if ((rc = verify(hb))) return done(rc);
+      if (hb.total == 0) {
+        k_out[0] = k.iwR;
+        k_out[1] = k.cR;
+        k_out[2] = k.iwL;
+        k_out[3] = k.cL;
+        k_out[4] = k.uhi;
+        *n_out = n;
+        return done(0);
       }
-      const uint32_t fa = fl(lo), fb = fl(hi);
-      if (hi - lo > 255 || ((fa >> 31) != (fb >> 31))) {
-        ok = false;
-        break;
+      if (pass == 1) break;
+      if ((rc = check(hipMemcpy(tab.data(), lut, 8 * (size_t)n, hipMemcpyDeviceToHost), "nqk_gelu_lut_build(read)")))
+        return done(rc);
+      bool ok = true;
+      for (int i = 0; i < n && ok; ++i) {
+        if (!hb.cnt[i]) continue;
+        auto fl = [](unsigned key) {  // key -> float bits
+          return (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+        };
+        auto key_of = [](uint32_t bits) { return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u); };
+        unsigned klo = hb.kmin[i], khi = hb.kmax[i];
+        const uint32_t thr = tab[i].x, K = (tab[i].y >> 8) & 0xffu;
+        const bool has_change = (tab[i].y & 0xffu) != ((tab[i].y >> 16) & 0xffu);
+        if (has_change) {  // the existing window in keys
+          const bool neg = thr >> 31;
+          const unsigned wa = neg ? key_of(thr + K) : key_of(thr), wb = neg ? key_of(thr) : key_of(thr + K);
+          klo = klo < wa ? klo : wa;
+          khi = khi > wb ? khi : wb;
+        }
+        const uint32_t fa = fl(klo), fb = fl(khi);
+        if (khi - klo > 255 || ((fa >> 31) != (fb >> 31))) {
+          ok = false;
+          break;
+        }
+        const bool neg = fa >> 31;
+        tab[i].x = neg ? fb : fa;
+        tab[i].y = (tab[i].y & 0xffff00ffu) | ((neg ? fa - fb : fb - fa) << 8);
       }
-      const bool neg = fa >> 31;
-      tab[i].x = neg ? fb : fa;
-      tab[i].y = (tab[i].y & 0xffff00ffu) | ((neg ? fa - fb : fb - fa) << 8);
+      if (!ok) break;
+      if ((rc = check(hipMemcpy(lut, tab.data(), 8 * (size_t)n, hipMemcpyHostToDevice), "nqk_gelu_lut_build(write)")))
+        return done(rc);
     }
-    if (!ok) break;
-    if ((rc = check(hipMemcpy(lut, tab.data(), 8 * (size_t)n, hipMemcpyHostToDevice), "nqk_gelu_lut_build(write)")))
-      return done(rc);
   }
   return done(0);  // *n_out = 0: the filtered chain stays
 }

@@ -1,1360 +1,10 @@
-// k_pg: the round-3 persistent projection GEMM of the fused ViT layer (the hot loop of
-// numpy_quantization.py:44-61 q_matmul for every act x W MatMul, with the consumer chain of
-// model.py:486-565 in the epilogue: QKV head split + quantize, FFN-up + GELU + quantize,
-// out-projection / FFN-down + bias + residual).
-//
-// Why this shape (measured on MI355X, tools/micro/fill.hip, tools/micro/xwave.hip,
-// profiles/r03_*):
-//  * v_mfma_i32_16x16x64_i8 sustains 3.9 POPS on random operands against 3.26 for the
-//    32x32x32 form: the chip holds ~1.95 GHz under it instead of ~1.6 (same cycles per op).
-//  * A SIMD overlaps one wave's MFMAs with VALU work (its own or another wave's) up to
-//    ~4-6 VALU per 32x32x32-equivalent; past that the VALU issue (≈4 cycles each) sets
-//    the pace.  The epilogues are VALU work, so: two independent 4-wave workgroups per CU
-//    (128 x 256 tiles), the second started half a tile later, so that one workgroup's
-//    epilogue runs beside the other's k loop; and epilogues with fewer VALU per element
-//    (zero-point column term as the MFMA's initial accumulator, one fma for the QKV
-//    rescale, a single measure per element for the rounding filter).
-//
-// Layout: 4 waves side by side along N, each 128 rows x 64 columns = 8 x 4 MFMA tiles of
-// 16 x 16 (acc[i][j], 4 registers).  The products are computed transposed (Bt fragment as
-// the MFMA's A operand), and the weight image stores the 64 columns of a wave permuted
-// (bperm), so that lane l holds, for M-subtile i, row 16 i + (l & 15) and the 16
-// CONSECUTIVE columns 16 (l >> 4) + 4 j + r: one 16-byte store per subtile (int8 outputs)
-// or four (f32), straight from the accumulators.
-// A [M][K] int8 (activations) and the tile-packed weight image both go HBM/L2 -> LDS by
-// buffer LDS-DMA into a 3-stage ring (24 KiB per 64-deep k-step); the 16-B chunks are
-// XOR-swizzled (sw) so the fragment reads are conflict-free ds_read_b128.  Every VMEM
-// operation of the loop is counted by compile-time vmcnt waits; LDS reads are inline asm
-// (a compiler-visible read of LDS-DMA'd bytes gets a vmcnt(0) that would drain the ring).
-#include <type_traits>
-
-#include "nqk_common.h"
-#include "nqk_numerics.h"
-#include "nqk_glut.h"
+// k_pg host side: the weight packers (nqk_pack_pg / nqk_pack_pg4) and the launcher; the
+// kernel is nqk_pgemm_kernel.h, its instantiations nqk_pg_inst_*.hip.
+#include "nqk_pgemm_kernel.h"
 
 namespace nqk {
-#if (NQK_PG_DIAG & 64)
-__device__ unsigned long long g_pg_slow[2];
-extern "C" unsigned long long nqk_pg_diag_slow(int reset) {
-  unsigned long long v[2] = {0, 0};
-  (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_pg_slow), sizeof(v));
-  const unsigned long long z[2] = {0, 0};
-  if (reset) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pg_slow), z, sizeof(z));
-  return v[0];
-}
-#endif
 namespace {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-typedef float v2f __attribute__((ext_vector_type(2)));
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-constexpr int PG_BM = 128, PG_BN = 256, PG_BK = 64, PG_RD = 3;
-constexpr int PG_ASTG = PG_BM * PG_BK;           // 8 KiB
-constexpr int PG_STG = PG_ASTG + PG_BN * PG_BK;  // 24 KiB
-constexpr int PG_COLP = PG_RD * PG_STG;          // 2 slots x (ct[256] int32 | bias[256] f32)
-constexpr int PG_LDS = PG_COLP + 2 * 2048;       // 76 KiB: two workgroups per CU
-constexpr int PG_PW = 2 + 4;                      // LDS-DMA pieces per wave per stage
-
-enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fused.hip
-constexpr int PG_GLUT = 5;  // GELU by table lookup (nqk_glut.h): launched for PG_GELU when a table is given
-// k_pg's LDS: a 3-stage ring of A (128 x 64 B) + B (256 rows x 64 B, or 32 B of int4
-// nibbles) per stage, the column constants (2 x 2 KiB), then the GELU table (PG_GLUT, 4 KiB)
-// or, for int4 weights, the residual epilogue's transpose scratch (int8: ring slot 2)
-constexpr int PG_TR_ROW = 272;  // bytes per staged residual row (256 + 16: conflict-free b128 writes)
-constexpr int pg_stg(bool b4) { return PG_ASTG + PG_BN * (b4 ? PG_BK / 2 : PG_BK); }
-constexpr int pg_colp(bool b4) { return PG_RD * pg_stg(b4); }
-constexpr int pg_lds_bytes(int epi, bool b4) {
-  return pg_colp(b4) + 4096 + (epi == PG_GLUT ? 8 * GLUT_MAX : 0) + (b4 && epi == PG_RESID ? 4 * 16 * PG_TR_ROW : 0);
-}
-
-#ifndef NQK_PG_STAUX
-#define NQK_PG_STAUX 2  // cache-policy bits of the epilogue's output stores: nt (profiles/r03c_*: out-proj
-                        // 77 -> 60 us; 16 = sc1, the line leaves L2: no gain)
-#endif
-#ifndef NQK_PG_STAUX_RESID
-#define NQK_PG_STAUX_RESID 0  // the residual epilogues' f32 output stores: plain, so the LayerNorm that
-                              // reads the rows next finds them in the Infinity Cache (same-box bench A/B,
-                              // profiles/r03_store_policy_ab.txt: LN 46.4 -> 42.1 us, residual GEMMs equal)
-#endif
-#ifndef NQK_PG_RLAUX
-#define NQK_PG_RLAUX -1  // cache-policy bits of the RESID epilogue's residual loads: -1 = nt for K = 3072
-                         // (FFN-down 144 -> 138 us) and plain for K = 768 (nt: out-proj 59 -> 70 us)
-#endif
-#ifndef NQK_PG_SPREAD
-#define NQK_PG_SPREAD 0  // 1: the stage's LDS-DMA pieces spread over the first half step (A/B variant)
-#endif
-#ifndef NQK_PG_GELU4
-#define NQK_PG_GELU4 1  // GELU epilogue two element pairs at a time, the chains interleaved
-#endif
-#ifndef NQK_PG_NOPK
-#define NQK_PG_NOPK 1  // 1: the QKV epilogue without packed f32 instructions (MI355X_MICROARCH.md:
-                       // beside MFMAs a v_pk_fma_f32 costs more than two v_fma_f32): QKV 97 -> 92 us
-#endif
-
-#ifndef NQK_PG_PRIO
-#define NQK_PG_PRIO 3  // 3: s_setprio 1 in the epilogue, 0 in the k loop (the epilogue's VALU ahead of the
-                       // other workgroup's k loop on the SIMD: -2..-4 %, profiles/r03c_*); 1: the reverse;
-                       // 2: static prio 1 for the second workgroup of a CU; 0: none
-#endif
-#ifndef NQK_PG_DIAG
-#define NQK_PG_DIAG 0  // diagnostic builds only (tools/pg_diag.sh): 1 = no epilogue stores,
-                       // 2 = trivial epilogue math, 4 = no operand loads, 8 = no barriers,
-                       // 16 = no fragment reads
-#endif
-
-// physical 16-B chunk of logical chunk c in 64-B LDS row r is c ^ pg_sw(r): the 16 lanes of
-// each ds_read_b128 lane group (rows 16 i + (l & 15), chunk l >> 4) then hit 16 different
-// 4-bank slots
-__host__ __device__ constexpr int pg_sw(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
-// column (within the wave's 64) held by the wave's LDS B row rw = 16 j + c.  Layout 0 (int8
-// outputs): lane (l & 15, lg = l >> 4) gets columns 16 lg + 4 j + r, 16 consecutive bytes;
-// layout 1 (f32 outputs): columns 16 j + 4 lg + r, so each 16-B store instruction j covers
-// 64 contiguous bytes of a row with the 4 lanes of that row
-__host__ __device__ constexpr int pg_bperm(int rw, int layout) {
-  return layout == 0 ? 16 * ((rw & 15) >> 2) + 4 * (rw >> 4) + (rw & 3) : rw;
-}
-
-template <int I>
-using ic = std::integral_constant<int, I>;
-template <int B, int E, typename F>
-__device__ __forceinline__ void sfor(F&& f) {
-  if constexpr (B < E) {
-    f(ic<B>{});
-    sfor<B + 1, E>(f);
-  }
-}
-
-__device__ __forceinline__ rsrc_t pg_rsrc(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ void pg_dma16(rsrc_t r, void* l, uint32_t voff, uint32_t soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)l, 16, voff, soff, 0, 0);
-}
-// LDS reads are compiler-visible (it places the lgkmcnt waits; an async load's destination
-// register must never be copied before its wait, which only the compiler can guarantee);
-// the compiler does not order them behind LDS-DMA, the explicit vmcnt waits + barriers do
-__device__ __forceinline__ v4i pg_lds16(const void* p) {
-  return *reinterpret_cast<const v4i*>(p);  // p points into the kernel's LDS array: ds_read_b128
-}
-// ds_read_b128 at base + a compile-time byte offset (the instruction's 16-bit offset field:
-// one address VGPR for every fragment read of the loop)
-#ifndef NQK_PG_ASMREAD
-#define NQK_PG_ASMREAD 0  // diagnostic: fragment reads by inline asm
-#endif
-template <int OFF>
-__device__ __forceinline__ v4i pg_lds16o(const int8_t* base) {
-  static_assert(OFF >= 0 && (OFF < 65536 || !NQK_PG_ASMREAD), "ds_read offset");
-  if constexpr (NQK_PG_ASMREAD) {
-    v4i v;
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"((uint32_t)(uintptr_t)(lds_ptr_t)base), "n"(OFF));
-    return v;
-  } else {
-    return *reinterpret_cast<const v4i*>(base + OFF);  // the offset folds into the instruction
-  }
-}
-// ds_read_b64 at base + a compile-time byte offset (the int4 weight fragments)
-template <int OFF>
-__device__ __forceinline__ v2u pg_lds8o(const int8_t* base) {
-  return *reinterpret_cast<const v2u*>(base + OFF);
-}
-__device__ __forceinline__ void pg_lgkm() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-// lgkmcnt(0) that the values read by pg_lds16 pass through: their uses cannot be moved
-// above the wait (a plain wait orders only memory operations)
-__device__ __forceinline__ void pg_lgkm_tie(v4i& a, v4i& b, v4i& c, v4i& d) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-__device__ __forceinline__ void pg_lgkm_tie_a4(v4i (&a)[4], v2u (&b)[4]) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-__device__ __forceinline__ void pg_lgkm_tie8(v4i (&a)[4], v4i (&b)[4]) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-template <int N>
-__device__ __forceinline__ void pg_vmcnt_tie(v4u (&a)[4]) {
-  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : "n"(N > 63 ? 63 : N) : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-template <int N>
-__device__ __forceinline__ void pg_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N > 63 ? 63 : N) : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-// 16-byte buffer load to VGPRs (compiler-visible: it places the vmcnt wait before the use)
-template <int AUX = 0>
-__device__ __forceinline__ v4u pg_load16(rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
-}
-__device__ __forceinline__ v4u pg_load16(rsrc_t r, uint32_t voff, uint32_t soff, int aux) {
-  return aux == 2 ? pg_load16<2>(r, voff, soff) : pg_load16<0>(r, voff, soff);
-}
-
-struct PgEpi {
-  float sacc[3];      // dequant scale per column group
-  float rsf[3];       // RN32(1 / s_out)
-  float c1[3];        // RN32(sacc * rsf)            (QKV fast path)
-  float k1[3];        // |c1| 6.25 2^-24             (QKV filter: rounding error per |v|)
-  float zp128[3];     // zp_out + 128 (f32)        (QKV: v_rndne + v_cvt_pk_u8 rounding)
-  float qlo[3], qhi[3], magic[3];  // lo - zp, hi - zp, 1.5 2^23 + zp (GELU: pg_round2)
-  float s_out[3];
-  double rs_out[3], zp_out[3];
-  void* out[3];
-  const float* bias;
-  const float* resid;
-  const int32_t* colterm;  // col[n] * zpa (int32)
-  double lo, hi;
-  int group_cols, tokens, heads, hdim;
-  float g_rel, g_lim;  // GELU filter (nqk_fused.hip make_epi)
-  float div, add1, mul2;
-  double rdiv;
-  int ldo;  // row stride (elements) of the GELU / RESID output
-  const void* lut;  // PG_GLUT: the GELU table (nqk_gelu_lut_build) and its bucket coordinate
-  GLutK gk;
-  float blo, bhi;   // QKV: the clamp of v + 128 ([lo + 128, hi + 128] of the bit width)
-};
-
-// quantize (numpy_quantization.py:24-34) with f64 zero-point add and clipping
-__device__ __forceinline__ int pg_quant_exact(float x, float s, double rs, double zp, double lo, double hi) {
-  (void)s;
-  const float t = (float)((double)x * rs);  // RN32(x / s) (s normal, host-checked)
-  const double u = zp + (double)t;
-  return (int)__builtin_rint(__builtin_fmin(__builtin_fmax(u, lo), hi));
-}
-
-// per-column-group constants of the exact fallback
-struct PgFix {
-  float c1, k1, rsf, sacc, lim, s_out;
-  double rs_out, zp;
-};
-// The rounding filter's exact fallback for element q of one epilogue step: recheck the
-// element's filter measure, and run the reference chain where it could not decide.
-// av: the int32 accumulators; xv: QKV the column bias, GELU h = RN(bias + RN(v sacc)).
-template <int EPI>
-__device__ __forceinline__ void pg_exact_fix1(int q, const int (&av)[16], const float (&xv)[16], uint32_t (&pk)[4],
-                                              const PgFix& f, const PgEpi& e) {
-  const float vf = (float)av[q];
-  const float x = xv[q];
-  bool slow;
-  if constexpr (EPI == PG_QKV) {
-    const float u = __builtin_fmaf(vf, f.c1, x * f.rsf);
-    const float r = __builtin_rintf(u);
-    slow = !(__builtin_fmaf(__builtin_fabsf(vf), f.k1, __builtin_fabsf(u - r)) < f.lim);
-  } else {
-    const float tf = gelu_fast(x) * f.rsf;
-    const float r = __builtin_rintf(tf);
-    slow = !(__builtin_fmaf(__builtin_fabsf(x), e.g_rel, __builtin_fabsf(tf - r)) < f.lim);
-  }
-  if (__any(slow)) {
-    if (slow) {
-      float y;
-      if constexpr (EPI == PG_QKV) {
-        y = x + vf * f.sacc;  // F32X: the f64 dequantize, exactly
-      } else {
-        y = x;
-        const float aa = ref_erf((float)((double)y * e.rdiv)) + e.add1;
-        y = (y * aa) * e.mul2;
-      }
-      const int qv = pg_quant_exact(y, f.s_out, f.rs_out, f.zp, e.lo, e.hi);
-      const int sh = 8 * (q & 3);
-      pk[q >> 2] = (pk[q >> 2] & ~(0xffu << sh)) | ((uint32_t)(qv & 0xff) << sh);
-    }
-  }
-}
-// ... for all 16 elements of the step (entered when any lane's worst measure fails).  GELU:
-// a loop that is not unrolled (av / xv / pk indexed by the wave-uniform q stay in VGPRs via
-// relative moves), so the long exact chain is not duplicated per element and per step; QKV:
-// unrolled (its exact chain is short; measured faster, profiles/r03_pg_micro.txt).
-// gm (QKV, and GELU with NQK_PG_GELU4): bit g set when some lane's filter measure of elements
-// 4 g .. 4 g + 3 failed; the other groups are skipped (their elements all passed)
-template <int EPI>
-__device__ __forceinline__ void pg_exact_fix(const int (&av)[16], const float (&xv)[16], uint32_t (&pk)[4],
-                                             const PgFix& f, const PgEpi& e, uint32_t gm = 15u) {
-  if constexpr (EPI == PG_QKV) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if ((gm >> g) & 1u) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pg_exact_fix1<EPI>(4 * g + j, av, xv, pk, f, e);
-      }
-    }
-  } else {
-#pragma clang loop unroll(disable)
-    for (int q = 0; q < 16; ++q) {
-      if ((gm >> (q >> 2)) & 1u) pg_exact_fix1<EPI>(q, av, xv, pk, f, e);
-    }
-  }
-}
-
-// gelu_fast (nqk_numerics.h) on two values with packed f32 arithmetic (v_pk_fma / v_pk_mul:
-// one instruction for both lanes of the pair, the same IEEE operations in the same order as
-// the scalar function, so the same bits: the epilogues are VALU-issue-bound and a packed
-// instruction issues at the scalar rate, tools/micro/valu.hip)
-__device__ __forceinline__ v2f gelu_fast2(v2f h) {
-  const v2f ah = __builtin_elementwise_abs(h);
-  const v2f d = __builtin_elementwise_fma(v2f{0.3275911f * 0.70710677f, 0.3275911f * 0.70710677f}, ah, v2f{1.0f, 1.0f});
-  const v2f t = v2f{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
-  v2f p = __builtin_elementwise_fma(v2f{0.5f * 1.061405429f, 0.5f * 1.061405429f}, t,
-                                    v2f{0.5f * -1.453152027f, 0.5f * -1.453152027f});
-  p = __builtin_elementwise_fma(p, t, v2f{0.5f * 1.421413741f, 0.5f * 1.421413741f});
-  p = __builtin_elementwise_fma(p, t, v2f{0.5f * -0.284496736f, 0.5f * -0.284496736f});
-  p = __builtin_elementwise_fma(p, t, v2f{0.5f * 0.254829592f, 0.5f * 0.254829592f});
-  const v2f ea = h * (h * v2f{-0.72134752f, -0.72134752f});
-  const v2f ex = v2f{__builtin_amdgcn_exp2f(ea[0]), __builtin_amdgcn_exp2f(ea[1])};
-  const v2f q = (p * t) * ex;
-  return __builtin_elementwise_fma(-ah, q, __builtin_elementwise_max(h, v2f{0.0f, 0.0f}));
-}
-
-// gelu_fast2 on two element pairs with every step of the two chains side by side: the
-// dependent packed instructions of one chain leave hazard wait states (s_nop) that the other
-// chain's instruction fills (same operations per lane, same bits)
-__device__ __forceinline__ void gelu_fast2x2(v2f h0, v2f h1, v2f& g0, v2f& g1) {
-  const v2f c1 = v2f{0.3275911f * 0.70710677f, 0.3275911f * 0.70710677f}, one = v2f{1.0f, 1.0f};
-  const v2f ah0 = __builtin_elementwise_abs(h0), ah1 = __builtin_elementwise_abs(h1);
-  const v2f d0 = __builtin_elementwise_fma(c1, ah0, one), d1 = __builtin_elementwise_fma(c1, ah1, one);
-  const v2f hc0 = h0 * v2f{-0.72134752f, -0.72134752f}, hc1 = h1 * v2f{-0.72134752f, -0.72134752f};
-  const v2f t0 = v2f{__builtin_amdgcn_rcpf(d0[0]), __builtin_amdgcn_rcpf(d0[1])};
-  const v2f t1 = v2f{__builtin_amdgcn_rcpf(d1[0]), __builtin_amdgcn_rcpf(d1[1])};
-  const v2f ea0 = h0 * hc0, ea1 = h1 * hc1;
-  const v2f k5 = v2f{0.5f * 1.061405429f, 0.5f * 1.061405429f}, k4 = v2f{0.5f * -1.453152027f, 0.5f * -1.453152027f};
-  const v2f k3 = v2f{0.5f * 1.421413741f, 0.5f * 1.421413741f}, k2 = v2f{0.5f * -0.284496736f, 0.5f * -0.284496736f};
-  const v2f k1 = v2f{0.5f * 0.254829592f, 0.5f * 0.254829592f};
-  v2f p0 = __builtin_elementwise_fma(k5, t0, k4), p1 = __builtin_elementwise_fma(k5, t1, k4);
-  const v2f ex0 = v2f{__builtin_amdgcn_exp2f(ea0[0]), __builtin_amdgcn_exp2f(ea0[1])};
-  const v2f ex1 = v2f{__builtin_amdgcn_exp2f(ea1[0]), __builtin_amdgcn_exp2f(ea1[1])};
-  p0 = __builtin_elementwise_fma(p0, t0, k3);
-  p1 = __builtin_elementwise_fma(p1, t1, k3);
-  p0 = __builtin_elementwise_fma(p0, t0, k2);
-  p1 = __builtin_elementwise_fma(p1, t1, k2);
-  p0 = __builtin_elementwise_fma(p0, t0, k1);
-  p1 = __builtin_elementwise_fma(p1, t1, k1);
-  const v2f pt0 = p0 * t0, pt1 = p1 * t1;
-  const v2f q0 = pt0 * ex0, q1 = pt1 * ex1;
-  const v2f z = v2f{0.0f, 0.0f};
-  g0 = __builtin_elementwise_fma(-ah0, q0, __builtin_elementwise_max(h0, z));
-  g1 = __builtin_elementwise_fma(-ah1, q1, __builtin_elementwise_max(h1, z));
-}
-
-// Q_LIM = (0.5 - 2^-126)(1 - 2^-23) rounded down: a rounded fma measure below it keeps the
-// exact one below 0.5 - 2^-126 (nqk_fused.hip quant_filter)
-constexpr float PG_QLIM = 0x1.fffffcp-2f;
-// QKV filter margin (round 4): |u - t| <= 6 units (2^-24) of |v c1| + 5 of |c2| to first order —
-// the roundings of c1 = RN(sacc rsf), rsf = RN(1/s) and the fma on the fast side, of v sacc,
-// + bias and / s_out on the reference's — so 6.25 and 5.25 units (round 3 used 8 and 16)
-#ifndef NQK_PG_QK1
-#define NQK_PG_QK1 0x1.9p-22f  // 6.25 2^-24 per |v c1|
-#endif
-#ifndef NQK_PG_QKC2
-#define NQK_PG_QKC2 0x1.5p-22f  // 5.25 2^-24 per |c2|
-#endif
-
-
-// B4: int4 weights (every value in [-8, 7]) as the nibble image of nqk_pack_pg4: a stage's
-// B part is 256 rows x 32 bytes (half the LDS-DMA pieces and LDS bytes); a lane's 16 k-values
-// of one MFMA operand are 8 bytes (ds_read_b64) that unpack with two AND masks into bytes
-// 16 w (the nibble in the high half, its sign bit on the byte's; as nqk_fused.hip
-// k_qgemm_big), so the MFMAs accumulate 16 acc exactly (initial accumulators 16 x the column
-// terms, host-checked to fit int32) and the epilogue takes acc >> 4.
-// S8 (QKV with 8-bit outputs): v_cvt_pk_u8_f32 saturates to [0, 255] (tools/micro/cvtu8.hip:
-// every integral f32 in [-2^24, 2^24], profiles/r04_cvtu8.txt), which is then the clamp, so the
-// v_med3 before it goes.
-template <int EPI, int NK, bool F32X, bool B4, bool S8 = false>
-__global__ void __launch_bounds__(256, 2)
-k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
-     PgEpi e) {
-  static_assert(NK % PG_RD == 0 && (NK >= 2 * PG_RD || NK == PG_RD), "k_pg: NK a multiple of the ring depth");
-  constexpr bool RESID = EPI == PG_RESID;
-  constexpr int BROW = B4 ? PG_BK / 2 : PG_BK;  // bytes of one B row per k-step
-  constexpr int NBP = B4 ? 2 : 4;               // B LDS-DMA pieces per wave per stage
-  constexpr int STG = pg_stg(B4), COLP = pg_colp(B4), LUTO = COLP + 4096;
-  constexpr int PW = 2 + NBP;                   // LDS-DMA pieces per wave per stage
-  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
-  const int l15 = lane & 15, lg = lane >> 4;
-
-  // tiles: the workgroups with blockIdx % 8 == x (one XCD under round-robin placement)
-  // walk the band [lo, hi) of tile ids, every nx-th tile from lo + jx; tile ids are
-  // row-panel major, so the tiles in flight on an XCD share A row panels in its L2.
-  const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X;
-  const int nx = (G - x + X - 1) / X;
-  const int lo = (int)((int64_t)ntiles * x / X), hi = (int)((int64_t)ntiles * (x + 1) / X);
-  const int first = lo + (int)(blockIdx.x / X);
-  const int iters = first < hi ? (hi - first + nx - 1) / nx : 0;
-  if (iters == 0) return;
-  auto tile_at = [&](int it) { return first + (it < iters ? it : iters - 1) * nx; };
-
-  constexpr int64_t BSTRIDE = (int64_t)NK * PG_BN * BROW;  // bytes of one column panel
-  const rsrc_t r_a = pg_rsrc(A, (uint32_t)((uint64_t)M * lda));
-  const rsrc_t r_b = pg_rsrc(Bp, (uint32_t)((uint64_t)tiles_n * BSTRIDE));
-  // LDS-DMA sources: A piece pp of wave w = rows 32 w + 16 pp + (l >> 2), physical chunk l & 3
-  const uint32_t va = (uint32_t)((32 * wave + (lane >> 2)) * lda + 16 * ((lane & 3) ^ pg_sw(lane >> 2)));
-  const uint32_t vb = (uint32_t)(NBP * 1024 * wave + 16 * lane);
-  // fragment offsets: row (l & 15) of a 16-row subtile, logical chunk l >> 4 (B4: 8-byte
-  // chunks of 32-byte rows, chunk ^ 2 in rows 8..15 of a subtile: conflict-free b64 reads)
-  const int f_off = l15 * 64 + 16 * (lg ^ pg_sw(l15));
-  const int f_off4 = l15 * 32 + 8 * (lg ^ (2 * ((l15 >> 3) & 1)));
-
-  struct Src { uint32_t sa, sb; int r0, tn; };
-  auto src_of = [&](int tile) __attribute__((always_inline)) {
-    Src s;
-    const int tm = tile / tiles_n;
-    s.tn = tile - tm * tiles_n;
-    // a ragged last tile row is computed as rows M - 128 .. M - 1 (the rows it shares
-    // with the tile above are written twice with the same values; host: out != resid)
-    s.r0 = tm * PG_BM < M - PG_BM ? tm * PG_BM : M - PG_BM;
-    s.sa = (uint32_t)s.r0 * (uint32_t)lda;
-    s.sb = (uint32_t)((int64_t)s.tn * BSTRIDE);
-    return s;
-  };
-  // LDS-DMA piece p of a stage (0, 1: A; 2 .. PW - 1: B)
-  auto issue_piece = [&](const Src& s, int kt, int slot, int p) __attribute__((always_inline)) {
-    if constexpr ((NQK_PG_DIAG & 4) != 0) return;
-    int8_t* st = lds + slot * STG;
-    if (p < 2) {
-      if constexpr ((NQK_PG_DIAG & 256) == 0)  // (diagnostic 256: no A pieces, 128: no B pieces)
-        pg_dma16(r_a, st + (2 * wave + p) * 1024, va, s.sa + (uint32_t)p * 16u * (uint32_t)lda + kt * PG_BK);
-    } else {
-      if constexpr ((NQK_PG_DIAG & 128) == 0)
-        pg_dma16(r_b, st + PG_ASTG + (NBP * wave + p - 2) * 1024, vb,
-                 s.sb + (uint32_t)(kt * (PG_BN * BROW) + (p - 2) * 1024));
-    }
-  };
-  auto issue_stage = [&](const Src& s, int kt, int slot) __attribute__((always_inline)) {
-#pragma unroll
-    for (int p = 0; p < PW; ++p) issue_piece(s, kt, slot, p);
-  };
-  // column constants of a tile (ct[256] | bias[256], 2 KiB): wave w moves bytes
-  // [512 w, 512 w + 512) with lanes 0..31 (one VMEM operation per wave, like every wave)
-  const rsrc_t r_ct = pg_rsrc(e.colterm, (uint32_t)((uint64_t)N * 4));
-  const rsrc_t r_bias = pg_rsrc(e.bias, e.bias ? (uint32_t)((uint64_t)N * 4) : 0u);
-  auto issue_colp = [&](int tn, int cslot) __attribute__((always_inline)) {
-    int8_t* dst = lds + COLP + cslot * 2048 + wave * 512;
-    const uint32_t voff = (uint32_t)((tn * PG_BN + (wave & 1) * 128 + (lane & 31) * 4) * 4);
-    if (lane < 32) {
-      if (wave < 2) pg_dma16(r_ct, dst, voff, 0);
-      else pg_dma16(r_bias, dst, voff, 0);  // bias == null: the descriptor returns zeros
-    }
-  };
-
-  v4i acc[8][4];
-  v4i a_lo[4], a_hi[4], b0[4], b1[4];
-  v2u p0[4], p1[4];  // B4: the packed fragments of the current / next step (b0 holds the unpacked ones)
-  const int8_t* const fa_base = lds + f_off;
-  const int8_t* const fb_base = B4 ? lds + f_off4 + 2048 * wave : fa_base + 4096 * wave;
-  // fragment reads: A subtile i (rows 16 i ..), B subtile j of the wave (rows 64 w + 16 j ..)
-  auto rd_a = [&](v4i (&dst)[4], auto SLOT, auto I0, auto Q) __attribute__((always_inline)) {
-    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
-    constexpr int q = decltype(Q)::value;
-    dst[q] = pg_lds16o<decltype(SLOT)::value * STG + (decltype(I0)::value + q) * 1024>(fa_base);
-  };
-  auto rd_b = [&](v4i (&dst)[4], auto SLOT, auto Q) __attribute__((always_inline)) {
-    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
-    constexpr int q = decltype(Q)::value;
-    dst[q] = pg_lds16o<decltype(SLOT)::value * STG + PG_ASTG + q * 1024>(fb_base);
-  };
-  // B4: 8 nibble bytes per fragment into the packed double buffer; unpack_b expands the
-  // current step's after its wait into b0 (the only unpacked set)
-  auto rd_b4 = [&](v2u (&dst)[4], auto SLOT, auto Q) __attribute__((always_inline)) {
-    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
-    constexpr int q = decltype(Q)::value;
-    dst[q] = pg_lds8o<decltype(SLOT)::value * STG + PG_ASTG + q * 512>(fb_base);
-  };
-  auto unpack_b = [&](const v2u (&p)[4]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      b0[q] = v4i{(int)((p[q][0] << 4) & 0xF0F0F0F0u), (int)(p[q][0] & 0xF0F0F0F0u), (int)((p[q][1] << 4) & 0xF0F0F0F0u),
-                  (int)(p[q][1] & 0xF0F0F0F0u)};
-  };
-  // 16 MFMAs of one half step (M-subtiles 4 h .. 4 h + 3) with fn(q) after MFMA q
-  auto half = [&](auto H, auto FIRST, const v4i (&aa)[4], const v4i (&bb)[4], const v4i (&ci)[4], auto&& fn)
-      __attribute__((always_inline)) {
-    constexpr int h = decltype(H)::value;
-    sfor<0, 16>([&](auto Q) __attribute__((always_inline)) {
-      constexpr int q = decltype(Q)::value, ii = q >> 2, j = q & 3;
-      if constexpr (decltype(FIRST)::value)
-        acc[4 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], ci[j], 0, 0, 0);
-      else
-        acc[4 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], acc[4 * h + ii][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      fn(Q);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-
-  // ---------------------------------------------------------------- epilogue of a tile
-  // rows r0 + 16 i + (l & 15), columns n0 + 64 w + 16 (l >> 4) + 0..15
-  auto epilogue = [&](const Src& s, int cslot) __attribute__((always_inline)) {
-    const int n0 = s.tn * PG_BN;
-    const int cw = n0 + 64 * wave;  // the wave's 64 columns: one head, one column group (host)
-    const int col0 = cw + 16 * lg;
-    const int8_t* cp = lds + COLP + cslot * 2048;
-    // PG_GLUT: LDS byte address of entry 0 minus bits(GLUT_MAGIC) * 8 (one v_lshl_add per lookup)
-    const uint32_t lut_base = (uint32_t)(uintptr_t)(lds_ptr_t)(lds + LUTO) - (GLUT_MAGIC_BITS << 3);
-    float bias[16];
-    {
-      v4i bb[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) bb[g] = pg_lds16(cp + 1024 + (64 * wave + 16 * lg + 4 * g) * 4);
-      pg_lgkm_tie(bb[0], bb[1], bb[2], bb[3]);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) bias[q] = __int_as_float(bb[q >> 2][q & 3]);
-    }
-    {
-      int g3 = 0;
-      if constexpr (EPI == PG_QKV) {
-        g3 = cw / e.group_cols;
-        g3 = g3 > 2 ? 2 : g3;
-      }
-      const float sacc = g3 == 0 ? e.sacc[0] : (g3 == 1 ? e.sacc[1] : e.sacc[2]);
-      const float rsf = g3 == 0 ? e.rsf[0] : (g3 == 1 ? e.rsf[1] : e.rsf[2]);
-      const float c1 = g3 == 0 ? e.c1[0] : (g3 == 1 ? e.c1[1] : e.c1[2]);
-      const float k1 = g3 == 0 ? e.k1[0] : (g3 == 1 ? e.k1[1] : e.k1[2]);
-      const float zp128 = g3 == 0 ? e.zp128[0] : (g3 == 1 ? e.zp128[1] : e.zp128[2]);
-      const float qlo = g3 == 0 ? e.qlo[0] : (g3 == 1 ? e.qlo[1] : e.qlo[2]);
-      const float qhi = g3 == 0 ? e.qhi[0] : (g3 == 1 ? e.qhi[1] : e.qhi[2]);
-      const float magic = g3 == 0 ? e.magic[0] : (g3 == 1 ? e.magic[1] : e.magic[2]);
-      const float s_out = g3 == 0 ? e.s_out[0] : (g3 == 1 ? e.s_out[1] : e.s_out[2]);
-      const double rs_out = g3 == 0 ? e.rs_out[0] : (g3 == 1 ? e.rs_out[1] : e.rs_out[2]);
-      const double zp = g3 == 0 ? e.zp_out[0] : (g3 == 1 ? e.zp_out[1] : e.zp_out[2]);
-      void* op = g3 == 0 ? e.out[0] : (g3 == 1 ? e.out[1] : e.out[2]);
-      // QKV: the head-layout buffer holds whole images, ceil(M / tokens) of them
-      // N % 256 != 0 (ViT-tiny): a wave whose 64 columns lie past N stores through a
-      // zero-size descriptor (dropped; its VMEM count stays that of every wave)
-      const rsrc_t r_out = pg_rsrc(
-          op, cw >= N ? 0u
-                      : (uint32_t)(EPI == PG_QKV ? (uint64_t)((M + e.tokens - 1) / e.tokens) * e.tokens * e.heads * e.hdim
-                                                 : (uint64_t)M * e.ldo));
-      // QKV: u = v c1 + c2 with c2 = RN(bias rsf): within |v| k1 + kb of zp + 128 + t,
-      // t = RN(RN(RN(v sacc) + bias) / s_out) (DESIGN.md §4.3 error bound); kb from the
-      // lane's largest |c2|, folded into the lane's limit
-      float c2[16];
-      float lim = PG_QLIM;
-      if constexpr (EPI == PG_QKV) {
-        float cm = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          c2[q] = bias[q] * rsf;
-          cm = __builtin_fmaxf(cm, __builtin_fabsf(c2[q]));
-        }
-        lim = (PG_QLIM - cm * NQK_PG_QKC2) - 0x1p-22f;  // conservative: every rounding down
-      } else {
-        lim = e.g_lim;
-      }
-      int hh = 0;
-      if constexpr (EPI == PG_QKV) hh = (cw - g3 * e.group_cols) / e.hdim;
-      sfor<0, 8>([&](auto I) __attribute__((always_inline)) {
-        constexpr int i = decltype(I)::value;
-        const int m = s.r0 + 16 * i + l15;
-        uint32_t off;
-        if constexpr (EPI == PG_QKV) {
-          const int img = m / e.tokens, t = m - img * e.tokens;
-          off = (uint32_t)(((img * e.heads + hh) * e.tokens + t) * e.hdim + 16 * lg);
-        } else {
-          off = (uint32_t)(m * e.ldo + col0);
-        }
-        if constexpr (EPI == PG_GLUT) {
-          // GELU by table lookup: h exactly as the reference (F32X), its bucket entry from
-          // the LDS table (one ds_read_b64 per element), the output byte selected by one
-          // compare (nqk_glut.h); no filter and no fallback path
-          float hv[16];
-          uint2 ent[16];
-#pragma unroll
-          for (int q = 0; q < 16; q += 2) {
-            const v4i& av4 = acc[i][q >> 2];
-            // (packed: the unpacked form measured 146 -> 157 us, profiles/r04_glut_unpacked_dropped.txt)
-            const v2f vf = v2f{(float)av4[q & 3], (float)av4[(q & 3) + 1]};
-            const v2f h = v2f{bias[q], bias[q + 1]} + vf * v2f{sacc, sacc};
-            const v2f r = __builtin_elementwise_fma(h, v2f{e.gk.iwR, e.gk.iwR}, v2f{e.gk.cR, e.gk.cR});
-            const v2f l = __builtin_elementwise_fma(h, v2f{e.gk.iwL, e.gk.iwL}, v2f{e.gk.cL, e.gk.cL});
-            hv[q] = h[0];
-            hv[q + 1] = h[1];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const float u = __builtin_amdgcn_fmed3f(__builtin_fmaxf(r[j], l[j]), GLUT_MAGIC, e.gk.uhi);
-              const uint32_t a = (__float_as_uint(u) << 3) + lut_base;
-              const v2u t = *(const __attribute__((address_space(3))) v2u*)(uintptr_t)a;
-              ent[q + j] = make_uint2(t[0], t[1]);
-            }
-          }
-          uint32_t pk[4] = {0, 0, 0, 0};
-          uint64_t slow = 0;  // lanes with an element in its entry's window
-          sfor<0, 16>([&](auto Q) __attribute__((always_inline)) {
-            constexpr int q = decltype(Q)::value;
-            pk[q >> 2] = glut_sel<q & 3>(pk[q >> 2], hv[q], ent[q].x, ent[q].y, slow);
-          });
-          if (__builtin_expect(slow != 0, 0) && (NQK_PG_DIAG & 32) == 0) {
-            // the exact chain for the elements inside a window (wave-uniform branch; a loop
-            // that is not unrolled keeps the chain's code once)
-            // (element q picked by compile-time selects: no runtime-indexed arrays, no scratch)
-#pragma clang loop unroll(disable)
-            for (int q = 0; q < 16; ++q) {
-              float hq = 0.0f;
-              uint32_t tq = 0u, iq = 0u;
-              sfor<0, 16>([&](auto Q) __attribute__((always_inline)) {
-                constexpr int c = decltype(Q)::value;
-                hq = q == c ? hv[c] : hq;
-                tq = q == c ? ent[c].x : tq;
-                iq = q == c ? ent[c].y : iq;
-              });
-              if (glut_in_window(hq, tq, iq)) {
-                const uint32_t qv =
-                    (uint32_t)glut_exact(hq, e.rdiv, e.add1, e.mul2, e.rs_out[0], e.zp_out[0], e.lo, e.hi) & 0xffu;
-                sfor<0, 4>([&](auto G) __attribute__((always_inline)) {
-                  constexpr int g = decltype(G)::value;
-                  const int sh = 8 * (q & 3);
-                  if ((q >> 2) == g) pk[g] = (pk[g] & ~(0xffu << sh)) | (qv << sh);
-                });
-              }
-            }
-          }
-          const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
-          if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-          else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, off, 0, NQK_PG_STAUX);
-          return;
-        }
-        uint32_t pk[4] = {0, 0, 0, 0};
-        uint32_t worst = 0;
-        uint32_t wgr[4] = {0, 0, 0, 0};  // QKV, GELU4: the measure's maximum per group of 4 elements
-        float hv[16];
-        v2f sprev;
-        // GELU, two pairs at a time (NQK_PG_GELU4): the two chains interleaved
-        if constexpr (EPI == PG_GELU && NQK_PG_GELU4 && (NQK_PG_DIAG & 2) == 0) {
-#pragma unroll
-          for (int q = 0; q < 16; q += 4) {
-            const v4i& av4 = acc[i][q >> 2];
-            const v2f vf0 = v2f{(float)av4[0], (float)av4[1]}, vf1 = v2f{(float)av4[2], (float)av4[3]};
-            const v2f h0 = v2f{bias[q], bias[q + 1]} + vf0 * v2f{sacc, sacc};
-            const v2f h1 = v2f{bias[q + 2], bias[q + 3]} + vf1 * v2f{sacc, sacc};
-            hv[q] = h0[0];
-            hv[q + 1] = h0[1];
-            hv[q + 2] = h1[0];
-            hv[q + 3] = h1[1];
-            v2f g0, g1;
-            gelu_fast2x2(h0, h1, g0, g1);
-            const v2f tf0 = g0 * v2f{rsf, rsf}, tf1 = g1 * v2f{rsf, rsf};
-            v2f dd0, dd1;
-            const v2f s0 = round_magic2(tf0, qlo, qhi, magic, dd0);
-            const v2f s1 = round_magic2(tf1, qlo, qhi, magic, dd1);
-            const float m0 = __builtin_fmaf(__builtin_fabsf(h0[0]), e.g_rel, __builtin_fabsf(dd0[0]));
-            const float m1 = __builtin_fmaf(__builtin_fabsf(h0[1]), e.g_rel, __builtin_fabsf(dd0[1]));
-            const float m2 = __builtin_fmaf(__builtin_fabsf(h1[0]), e.g_rel, __builtin_fabsf(dd1[0]));
-            const float m3 = __builtin_fmaf(__builtin_fabsf(h1[1]), e.g_rel, __builtin_fabsf(dd1[1]));
-            wgr[q >> 2] = __builtin_elementwise_max(__builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)),
-                                                    __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3)));
-            worst = __builtin_elementwise_max(worst, wgr[q >> 2]);
-            pk[q >> 2] = pack4_low(s0, s1);
-          }
-        }
-        // the fast paths on element pairs (packed f32 arithmetic where an instruction exists)
-#pragma unroll
-        for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) == 0 && !(EPI == PG_GELU && NQK_PG_GELU4); q += 2) {
-          const v2f vf = v2f{(float)acc[i][q >> 2][q & 3], (float)acc[i][q >> 2][(q & 3) + 1]};
-          v2f dd, sv;
-          float m0, m1;
-          if constexpr (EPI == PG_QKV) {  // (pg_round2 measured slower here: a longer dependent chain)
-            v2f u, rr, b;
-            if constexpr (NQK_PG_NOPK) {  // the same IEEE operations per element, unpacked
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                u[j] = __builtin_fmaf(vf[j], c1, c2[q + j]);
-                rr[j] = __builtin_rintf(u[j]);
-                dd[j] = u[j] - rr[j];
-                b[j] = rr[j] + zp128;
-              }
-            } else {
-              u = __builtin_elementwise_fma(vf, v2f{c1, c1}, v2f{c2[q], c2[q + 1]});
-              rr = v2f{__builtin_rintf(u[0]), __builtin_rintf(u[1])};
-              dd = u - rr;
-              b = rr + v2f{zp128, zp128};
-            }
-            m0 = __builtin_fmaf(__builtin_fabsf(vf[0]), k1, __builtin_fabsf(dd[0]));
-            m1 = __builtin_fmaf(__builtin_fabsf(vf[1]), k1, __builtin_fabsf(dd[1]));
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(S8 ? b[0] : __builtin_amdgcn_fmed3f(b[0], e.blo, e.bhi), q & 3,
-                                                        pk[q >> 2]);
-            pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(S8 ? b[1] : __builtin_amdgcn_fmed3f(b[1], e.blo, e.bhi),
-                                                        (q & 3) + 1, pk[q >> 2]);
-          } else {  // GELU: h exactly as the reference (F32X), then the filtered fast chain
-            const v2f h = v2f{bias[q], bias[q + 1]} + vf * v2f{sacc, sacc};
-            hv[q] = h[0];
-            hv[q + 1] = h[1];
-            const v2f tf = gelu_fast2(h) * v2f{rsf, rsf};
-            sv = round_magic2(tf, qlo, qhi, magic, dd);
-            m0 = __builtin_fmaf(__builtin_fabsf(h[0]), e.g_rel, __builtin_fabsf(dd[0]));
-            m1 = __builtin_fmaf(__builtin_fabsf(h[1]), e.g_rel, __builtin_fabsf(dd[1]));
-          }
-          if constexpr (EPI == PG_QKV)
-            wgr[q >> 2] = __builtin_elementwise_max(wgr[q >> 2], __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
-          else
-            worst = __builtin_elementwise_max(worst, __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
-          if constexpr (EPI != PG_QKV) {
-            if (q & 2) pk[q >> 2] = pack4_low(sprev, sv);
-            sprev = sv;
-          }
-        }
-        if constexpr (EPI == PG_QKV) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) pk[g] ^= 0x80808080u;  // offset bytes to two's complement
-          worst = __builtin_elementwise_max(__builtin_elementwise_max(wgr[0], wgr[1]),
-                                            __builtin_elementwise_max(wgr[2], wgr[3]));
-        }
-#pragma unroll
-        for (int q = 0; q < 16 && (NQK_PG_DIAG & 2) != 0; ++q)  // diagnostic: no epilogue math
-          pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32((float)(acc[i][q >> 2][q & 3] & 255), q & 3, pk[q >> 2]);
-        if constexpr ((NQK_PG_DIAG & 34) == 0) {  // (diagnostic 32: no exact fallback)
-          if (__builtin_expect(__any(worst >= __float_as_uint(lim)), 0)) {
-#if (NQK_PG_DIAG & 64)
-            if (lane == 0) atomicAdd(&g_pg_slow[0], 1ull);  // diagnostic: count exact-path entries
-#endif
-            int av[16];
-            float xv[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-              av[q] = acc[i][q >> 2][q & 3];
-              xv[q] = EPI == PG_QKV ? bias[q] : hv[q];
-            }
-            uint32_t gm = 15u;
-            if constexpr (EPI == PG_QKV || (EPI == PG_GELU && NQK_PG_GELU4)) {
-              gm = 0u;
-#pragma unroll
-              for (int g = 0; g < 4; ++g) gm |= __any(wgr[g] >= __float_as_uint(lim)) ? 1u << g : 0u;
-            }
-            pg_exact_fix<EPI>(av, xv, pk, PgFix{c1, k1, rsf, sacc, lim, s_out, rs_out, zp}, e, gm);
-          }
-        }
-        const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
-        if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, off, 0, NQK_PG_STAUX);
-      });
-    }
-  };
-
-  // RESID epilogue: y = (bias + RN(v sacc)) + residual, f32 stores, with whole 128-B lines
-  // per instruction: each subtile's accumulators go through the wave's part of ring slot 2
-  // (free from the barrier after the k loop until the next tile's step 0 refills it), row-
-  // major [16 rows][64 columns] int32 with 272-B rows, and come back transposed: lane
-  // (a = l & 15, b = l >> 4) takes row 4 k + b, columns 4 a .. 4 a + 3 for k = 0..3, so the
-  // 16 lanes of a row load / store its 256 contiguous bytes.  Residual loads of subtile i + 2
-  // are issued after subtile i's stores (0 and 1 before the next tile's stages); the
-  // compiler places their waits (compiler-visible loads).
-  const rsrc_t r_res = pg_rsrc(RESID ? e.resid : nullptr, RESID ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
-  const rsrc_t r_nul = pg_rsrc(RESID ? e.resid : nullptr, 0u);  // columns past N: loads return 0, stores drop
-  constexpr int TR_ROW = PG_TR_ROW;
-  int8_t* const tr = lds + (B4 ? COLP + 4096 : 2 * STG) + wave * (16 * TR_ROW);
-  const int ta = lane & 15, tb = lane >> 4;
-  v4u resv[3][4];
-  auto res_off = [&](const Src& s, int i, int k) __attribute__((always_inline)) {
-    return (uint32_t)(((s.r0 + 16 * i + 4 * k + tb) * e.ldo + s.tn * PG_BN + 64 * wave + 4 * ta) * 4);
-  };
-  auto res_issue = [&](const Src& s, auto I) __attribute__((always_inline)) {
-    constexpr int i = decltype(I)::value;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      resv[i % 3][k] = pg_load16(s.tn * PG_BN + 64 * wave < N ? r_res : r_nul, res_off(s, i, k), 0u,
-                                 NQK_PG_RLAUX >= 0 ? NQK_PG_RLAUX : (NK == 48 ? 2 : 0));
-  };
-  auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
-    const int8_t* cp = lds + COLP + cslot * 2048;
-    const v4i bb = pg_lds16(cp + 1024 + (64 * wave + 4 * ta) * 4);  // columns 4 a .. 4 a + 3
-    const v2f b01 = v2f{__int_as_float(bb[0]), __int_as_float(bb[1])};
-    const v2f b23 = v2f{__int_as_float(bb[2]), __int_as_float(bb[3])};
-    const rsrc_t r_out = pg_rsrc(e.out[0], s.tn * PG_BN + 64 * wave < N ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
-    const float sacc = e.sacc[0];
-    sfor<0, 8>([&](auto I) __attribute__((always_inline)) {
-      constexpr int i = decltype(I)::value;
-      // this lane's 16 accumulators: row l15, columns 16 j + 4 lg + r (layout 1)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) *reinterpret_cast<v4i*>(tr + l15 * TR_ROW + (16 * j + 4 * lg) * 4) = acc[i][j];
-      v4i t[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) t[k] = *reinterpret_cast<const v4i*>(tr + (4 * k + tb) * TR_ROW + 16 * ta);
-      const v4u(&rv)[4] = resv[i % 3];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v4u st;
-        if constexpr (F32X) {  // (unpacked: within noise, profiles/r04_qkv_nopk_ab.txt)
-          const v2f d01 = v2f{(float)t[k][0], (float)t[k][1]} * v2f{sacc, sacc};
-          const v2f d23 = v2f{(float)t[k][2], (float)t[k][3]} * v2f{sacc, sacc};
-          const v2f y01 = (b01 + d01) + v2f{__uint_as_float(rv[k][0]), __uint_as_float(rv[k][1])};
-          const v2f y23 = (b23 + d23) + v2f{__uint_as_float(rv[k][2]), __uint_as_float(rv[k][3])};
-          st = v4u{__float_as_uint(y01[0]), __float_as_uint(y01[1]), __float_as_uint(y23[0]), __float_as_uint(y23[1])};
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float d = (float)((double)t[k][r] * (double)sacc);
-            st[r] = __float_as_uint((__int_as_float(bb[r]) + d) + __uint_as_float(rv[k][r]));
-          }
-        }
-        if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, res_off(s, i, k), 0, NQK_PG_STAUX_RESID);
-      }
-      if constexpr (i + 2 < 8) res_issue(s, ic<i + 2>{});
-    });
-  };
-
-  // ---------------------------------------------------------------- the persistent loop
-  // VMEM operations per wave, in issue order: [colp(next)] at step 1; stage kt + 2 in step
-  // kt's first half; after the k loop (RESID: residual of subtiles 0, 1), the next tile's
-  // stages 0 and 1, then the epilogue's operations (EOPS)
-  // RESID: 8 x 4 stores after the stages (counted conservatively without the 6 x 4 residual
-  // loads, which the compiler may hoist above the stage issues: a smaller count only waits more)
-  constexpr int EOPS = RESID ? 32 : 8;
-  constexpr int PWA = PW;
-  Src cur = src_of(tile_at(0));
-  // PG_GLUT: the 4 KiB GELU table into LDS, 1 KiB per wave (waited for with stage 0)
-  if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
-  issue_colp(cur.tn, 0);
-  issue_stage(cur, 0, 0);
-  issue_stage(cur, 1, 1);
-  if constexpr (NQK_PG_PRIO == 2) {
-    if ((int)blockIdx.x >= G / 2) __builtin_amdgcn_s_setprio(1);
-  }
-  for (int it = 0; it < iters; ++it) {
-    if constexpr (NQK_PG_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-    if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(0);
-    const bool more = it + 1 < iters;
-    const Src nxt = src_of(tile_at(more ? it + 1 : it));
-    const int cs = it & 1;
-    // stage 0 and this tile's column constants landed (younger: stage 1, the previous
-    // epilogue's operations)
-    if (it == 0) pg_vmcnt<PWA>();
-    else pg_vmcnt<PWA + EOPS>();
-    if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    // initial accumulators: minus the zero-point column terms of the lane's 16 columns
-    v4i cinit[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      cinit[j] = pg_lds16(lds + COLP + cs * 2048 + (64 * wave + (RESID ? 16 * j + 4 * lg : 16 * lg + 4 * j)) * 4);
-    sfor<0, 4>([&](auto Q) __attribute__((always_inline)) {
-      rd_a(a_lo, ic<0>{}, ic<0>{}, Q);
-      if constexpr (B4) rd_b4(p0, ic<0>{}, Q);
-      else rd_b(b0, ic<0>{}, Q);
-    });
-    if constexpr (B4) {
-      pg_lgkm_tie_a4(a_lo, p0);
-      unpack_b(p0);
-    } else {
-      pg_lgkm_tie8(a_lo, b0);
-    }
-    pg_lgkm_tie(cinit[0], cinit[1], cinit[2], cinit[3]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cinit[j] = B4 ? -(cinit[j] << 4) : -cinit[j];
-    sfor<0, NK>([&](auto KT) __attribute__((always_inline)) {
-      constexpr int kt = decltype(KT)::value;
-      constexpr int slot = kt % PG_RD;
-      v4i(&bc)[4] = B4 ? b0 : ((kt & 1) ? b1 : b0);
-      v4i(&bn)[4] = (kt & 1) ? b0 : b1;
-      v2u(&pc)[4] = (kt & 1) ? p1 : p0;
-      v2u(&pn)[4] = (kt & 1) ? p0 : p1;
-      if constexpr (kt > 0) {  // this step's fragments (read in step kt - 1)
-        if constexpr (B4) {
-          pg_lgkm_tie_a4(a_lo, pc);
-          unpack_b(pc);
-        } else {
-          pg_lgkm_tie8(a_lo, bc);
-        }
-      }
-      // first half: subtiles 0..3; between the MFMAs the second half's A fragments and the
-      // refill of the slot step kt - 1 read (stage kt + 2)
-      half(ic<0>{}, std::integral_constant<bool, kt == 0>{}, a_lo, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
-        constexpr int q = decltype(Q)::value;
-        if constexpr (q < 4) rd_a(a_hi, ic<slot>{}, ic<4>{}, Q);
-        // stage kt + 2: NQK_PG_SPREAD 0 = all pieces after MFMA 4; 1 = one piece every
-        // other MFMA from MFMA 1 (a burst of LDS-DMA issues costs each piece more:
-        // MI355X_MICROARCH.md, LDS-DMA piece issue cost)
-        if constexpr (kt + 2 < NK) {
-          if constexpr (NQK_PG_SPREAD == 0) {
-            if constexpr (q == 4) issue_stage(cur, kt + 2, (kt + 2) % PG_RD);
-          } else if constexpr ((q & 1) == 1 && (q >> 1) < PW) {
-            issue_piece(cur, kt + 2, (kt + 2) % PG_RD, q >> 1);
-          }
-        }
-      });
-      if constexpr (kt == 1) issue_colp(nxt.tn, cs ^ 1);
-      if constexpr (kt + 1 < NK) {
-        // stage kt + 1 landed; younger: stage kt + 2 (if issued), colp (step 1), and for
-        // stage 1 the previous tile's epilogue operations
-        constexpr int y = (kt + 2 < NK ? PWA : 0) + ((kt == 1 || kt == 2) ? 1 : 0);
-        if (kt == 0 && it > 0) pg_vmcnt<y + EOPS>();
-        else pg_vmcnt<y>();
-        pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
-        if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
-      }
-      half(ic<1>{}, std::integral_constant<bool, kt == 0>{}, a_hi, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
-        constexpr int q = decltype(Q)::value;
-        if constexpr (kt + 1 < NK) {
-          if constexpr (q < 4) rd_a(a_lo, ic<(kt + 1) % PG_RD>{}, ic<0>{}, Q);
-          else if constexpr (q < 8) {
-            if constexpr (B4) rd_b4(pn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
-            else rd_b(bn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
-          }
-        }
-      });
-    });
-    // RESID: the residual rows of the first two subtiles, then the next tile's first
-    // stages (slots 0 and 1: last read before step NK - 2's barrier); a barrier frees slot 2
-    // (stage NK - 1) for the epilogue's transposes
-    if constexpr (RESID) {
-      res_issue(cur, ic<0>{});
-      res_issue(cur, ic<1>{});
-      if constexpr (!B4) __builtin_amdgcn_s_barrier();  // (B4: the scratch is not in the ring)
-    }
-    // (the last tile re-stages its own first stages: never read, drained at the end; the
-    // VMEM counts stay the same on every path)
-    issue_stage(nxt, 0, 0);
-    issue_stage(nxt, 1, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (NQK_PG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-    if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(1);
-    if constexpr (B4) {  // the MFMAs accumulated 16 acc
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = acc[i][j] >> 4;
-    }
-    if constexpr (RESID) epilogue_resid(cur, cs);
-    else epilogue(cur, cs);
-    cur = nxt;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---------------------------------------------------------------------------------------
-// k_pg2: the epilogue of tile t - 1 runs INSIDE the k loop of tile t, in the same waves'
-// instruction streams (a SIMD overlaps a wave's own VALU with its MFMAs: tools/micro/fill.hip
-// 16x16x64 with 12 VALU per 32x32x32-equivalent runs at 0.55 of the MFMA-only rate, where the
-// two run back to back at ~0.35).  One 512-thread workgroup per CU, 8 waves as 2 (M) x 4 (N),
-// each 64 x 64 of a 128 x 256 tile: 64 accumulator registers for tile t and 64 holding tile
-// t - 1's results.  The A / B ring (4 stages of 24 KiB) runs continuously across tiles.
-// Per wave the epilogue is 4 units (M-subtiles of 16 rows x the wave's 64 columns, 16 values
-// per lane); unit u of tile t - 1 is spread over k steps SPU u .. SPU u + SPU - 1 of tile t
-// (SPU = NK / 4) in element pairs, its store at the end of its last step, the rounding
-// filter's exact fallback (rare, a wave-uniform branch) right after.  The first tile's k loop
-// runs the epilogue on no data through zero-size buffer descriptors (loads return 0, stores
-// are dropped); the last tile's epilogue runs after the loop.
-constexpr int P2_RD = 4, P2_PW = 3;             // ring stages; LDS-DMA ops per wave per stage
-constexpr int P2_COLP = P2_RD * PG_STG;         // 3 slots x (ct[256] | bias[256])
-constexpr int P2_TRS = P2_COLP + 3 * 2048;      // RESID: per-wave transpose scratch
-constexpr int P2_TR_ROW = 272;
-constexpr int p2_lds(int epi) { return P2_TRS + (epi == PG_RESID ? 8 * 16 * P2_TR_ROW : 0); }
-
-template <int EPI, int NK>
-struct P2Sched {  // the static per-k-step schedule (unit, phase, pairs per half)
-  static constexpr int SPU = NK / 4;
-  static constexpr int unit(int kt) { return kt / SPU; }
-  static constexpr int ph(int kt) { return kt % SPU; }
-  // element pairs [lo, hi) of the unit handled in half h (0 / 1) of step kt
-  static constexpr int plo(int kt, int h) { return 8 * (2 * ph(kt) + h) / (2 * SPU); }
-  static constexpr int phi(int kt, int h) { return 8 * (2 * ph(kt) + h + 1) / (2 * SPU); }
-  static constexpr bool last(int kt) { return ph(kt) == SPU - 1; }
-  // VMEM operations of the step besides the half-1 LDS-DMA: colp (step 1, start of half 2),
-  // RESID residual loads (phase 0, half 2), the unit's stores (last phase, half 2)
-  static constexpr int half2_ops(int kt) {
-    return (kt == 1 ? 1 : 0) + (EPI == PG_RESID && ph(kt) == 0 ? 4 : 0) + (last(kt) ? (EPI == PG_RESID ? 4 : 1) : 0);
-  }
-  static constexpr int m(int k) { return ((k % NK) + NK) % NK; }
-  // ops younger than stage g + 1 (issued in half 1 of step g - 2) at the middle of step g
-  static constexpr int younger(int kt) {
-    return half2_ops(m(kt - 2)) + P2_PW + half2_ops(m(kt - 1)) + P2_PW;
-  }
-};
-
-template <int EPI, int NK, bool F32X>
-__global__ void __launch_bounds__(512, 1)
-k_pg2(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
-      PgEpi e) {
-  static_assert(NK % P2_RD == 0 && NK % 4 == 0 && NK >= 8, "k_pg2: NK");
-  using S = P2Sched<EPI, NK>;
-  constexpr bool RESID = EPI == PG_RESID;
-  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int l15 = lane & 15, lg = lane >> 4;
-
-  const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X, jx = blockIdx.x / X;
-  const int nx = (G - x + X - 1) / X;
-  const int lo = (int)((int64_t)ntiles * x / X), hi = (int)((int64_t)ntiles * (x + 1) / X);
-  const int first = lo + jx;
-  if (first >= hi) return;
-  const int cnt = (hi - first + nx - 1) / nx;
-
-  constexpr int64_t BSTRIDE = (int64_t)NK * PG_BN * PG_BK;
-  const rsrc_t r_a = pg_rsrc(A, (uint32_t)((uint64_t)M * lda));
-  const rsrc_t r_b = pg_rsrc(Bp, (uint32_t)((uint64_t)tiles_n * BSTRIDE));
-  // LDS-DMA: A piece = wave (rows 16 w .. 16 w + 15), B pieces 2 w, 2 w + 1
-  const uint32_t va = (uint32_t)((16 * wave + (lane >> 2)) * lda + 16 * ((lane & 3) ^ pg_sw(lane >> 2)));
-  const uint32_t vb = (uint32_t)(2048 * wave + 16 * lane);
-  const int f_off = l15 * 64 + 16 * (lg ^ pg_sw(l15));
-
-  struct Src { uint32_t sa, sb; int r0, tn; };
-  auto src_of = [&](int it) __attribute__((always_inline)) {
-    Src s;
-    const int tile = first + (it < cnt ? it : cnt - 1) * nx;
-    const int tm = tile / tiles_n;
-    s.tn = tile - tm * tiles_n;
-    s.r0 = tm * PG_BM < M - PG_BM ? tm * PG_BM : M - PG_BM;
-    s.sa = (uint32_t)s.r0 * (uint32_t)lda;
-    s.sb = (uint32_t)((int64_t)s.tn * BSTRIDE);
-    return s;
-  };
-  auto issue_stage = [&](const Src& s, int kt, int slot) __attribute__((always_inline)) {
-    if constexpr ((NQK_PG_DIAG & 4) != 0) return;
-    int8_t* st = lds + slot * PG_STG;
-    pg_dma16(r_a, st + wave * 1024, va, s.sa + kt * PG_BK);
-    pg_dma16(r_b, st + PG_ASTG + (2 * wave) * 1024, vb, s.sb + (uint32_t)(kt * (PG_BN * PG_BK)));
-    pg_dma16(r_b, st + PG_ASTG + (2 * wave + 1) * 1024, vb, s.sb + (uint32_t)(kt * (PG_BN * PG_BK) + 1024));
-  };
-  // column constants of a tile (ct[256] | bias[256]): 256 B per wave, lanes 0..15
-  const rsrc_t r_ct = pg_rsrc(e.colterm, (uint32_t)((uint64_t)N * 4));
-  const rsrc_t r_bias = pg_rsrc(e.bias, e.bias ? (uint32_t)((uint64_t)N * 4) : 0u);
-  auto issue_colp = [&](int tn, int cslot) __attribute__((always_inline)) {
-    int8_t* dst = lds + P2_COLP + cslot * 2048 + wave * 256;
-    const uint32_t voff = (uint32_t)((tn * PG_BN + (wave & 3) * 64 + (lane & 15) * 4) * 4);
-    if (lane < 16) {
-      if (wave < 4) pg_dma16(r_ct, dst, voff, 0);
-      else pg_dma16(r_bias, dst, voff, 0);
-    }
-  };
-
-  v4i acc[4][4], accp[4][4];
-  v4i a01[2], a23[2], b0[4], b1[4], cinit[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) accp[i][j] = v4i{0, 0, 0, 0};
-  const int8_t* const fa_base = lds + f_off + wm * 4096;
-  const int8_t* const fb_base = lds + f_off + wn * 4096;
-  auto rd_a = [&](v4i (&dst)[2], auto SLOT, auto I0, auto Q) __attribute__((always_inline)) {
-    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
-    constexpr int q = decltype(Q)::value;
-    dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + (decltype(I0)::value + q) * 1024>(fa_base);
-  };
-  auto rd_b = [&](v4i (&dst)[4], auto SLOT, auto Q) __attribute__((always_inline)) {
-    if constexpr ((NQK_PG_DIAG & 16) != 0) return;
-    constexpr int q = decltype(Q)::value;
-    dst[q] = pg_lds16o<decltype(SLOT)::value * PG_STG + PG_ASTG + q * 1024>(fb_base);
-  };
-  auto rd_cinit = [&](int cslot) __attribute__((always_inline)) {
-    const int8_t* cp = lds + P2_COLP + cslot * 2048;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      cinit[j] = pg_lds16(cp + (64 * wn + (RESID ? 16 * j + 4 * lg : 16 * lg + 4 * j)) * 4);
-  };
-
-  // ------------------------------------------------------------ the epilogue's state
-  // per tile (of tile t - 1, set at tile t's start): output descriptor (zero-size on the
-  // first tile), per-lane column constants, per-unit packed bytes / worst measure
-  struct EpiT {
-    rsrc_t out, res;
-    int r0, n0, g3;
-    float sacc, rsf, c1, k1, zp128, qlo, qhi, magic, lim;
-    int hh;
-  };
-  float ecol[16];  // QKV: c2 = RN(bias rsf); GELU: bias; RESID: bias of columns 4 ta .. + 3
-  uint32_t pk[4];
-  uint32_t worst = 0;
-  float hv[16];
-  v2f sprev;
-  v4u resv[4];
-  int8_t* const tr = lds + P2_TRS + wave * (16 * P2_TR_ROW);
-  const int ta = lane & 15, tb = lane >> 4;
-
-  auto epi_setup = [&](const Src& s, int cslot, bool valid) __attribute__((always_inline)) {
-    EpiT t;
-    t.r0 = s.r0;
-    t.n0 = s.tn * PG_BN;
-    const int cw = t.n0 + 64 * wn;
-    int g3 = 0;
-    if constexpr (EPI == PG_QKV) {
-      g3 = cw / e.group_cols;
-      g3 = g3 > 2 ? 2 : g3;
-    }
-    t.g3 = g3;
-    t.sacc = g3 == 0 ? e.sacc[0] : (g3 == 1 ? e.sacc[1] : e.sacc[2]);
-    t.rsf = g3 == 0 ? e.rsf[0] : (g3 == 1 ? e.rsf[1] : e.rsf[2]);
-    t.c1 = g3 == 0 ? e.c1[0] : (g3 == 1 ? e.c1[1] : e.c1[2]);
-    t.k1 = g3 == 0 ? e.k1[0] : (g3 == 1 ? e.k1[1] : e.k1[2]);
-    t.zp128 = g3 == 0 ? e.zp128[0] : (g3 == 1 ? e.zp128[1] : e.zp128[2]);
-    t.qlo = g3 == 0 ? e.qlo[0] : (g3 == 1 ? e.qlo[1] : e.qlo[2]);
-    t.qhi = g3 == 0 ? e.qhi[0] : (g3 == 1 ? e.qhi[1] : e.qhi[2]);
-    t.magic = g3 == 0 ? e.magic[0] : (g3 == 1 ? e.magic[1] : e.magic[2]);
-    void* op = g3 == 0 ? e.out[0] : (g3 == 1 ? e.out[1] : e.out[2]);
-    uint32_t obytes;
-    if constexpr (EPI == PG_QKV) obytes = (uint32_t)((uint64_t)((M + e.tokens - 1) / e.tokens) * e.tokens * e.heads * e.hdim);
-    else if constexpr (RESID) obytes = (uint32_t)((uint64_t)M * e.ldo * 4);
-    else obytes = (uint32_t)((uint64_t)M * e.ldo);
-    t.out = pg_rsrc(op, valid ? obytes : 0u);
-    t.res = pg_rsrc(RESID ? e.resid : nullptr, RESID && valid ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
-    t.hh = EPI == PG_QKV ? (cw - g3 * e.group_cols) / e.hdim : 0;
-    const int8_t* cp = lds + P2_COLP + cslot * 2048 + 1024;
-    if constexpr (RESID) {
-      const v4i bb = pg_lds16(cp + (64 * wn + 4 * ta) * 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ecol[r] = __int_as_float(bb[r]);
-      t.lim = 0.0f;
-    } else {
-      v4i bb[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) bb[g] = pg_lds16(cp + (64 * wn + 16 * lg + 4 * g) * 4);
-      float cm = 0.0f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float b = __int_as_float(bb[q >> 2][q & 3]);
-        if constexpr (EPI == PG_QKV) {
-          ecol[q] = b * t.rsf;
-          cm = __builtin_fmaxf(cm, __builtin_fabsf(ecol[q]));
-        } else {
-          ecol[q] = b;
-        }
-      }
-      t.lim = EPI == PG_QKV ? (PG_QLIM - cm * NQK_PG_QKC2) - 0x1p-22f : e.g_lim;
-    }
-    return t;
-  };
-  // output offset of unit u's row (QKV: head layout; GELU: row-major int8)
-  auto unit_off = [&](const EpiT& t, int u) __attribute__((always_inline)) {
-    const int m = t.r0 + 64 * wm + 16 * u + l15;
-    if constexpr (EPI == PG_QKV) {
-      const int img = m / e.tokens, tt = m - img * e.tokens;
-      return (uint32_t)(((img * e.heads + t.hh) * e.tokens + tt) * e.hdim + 16 * lg);
-    } else {
-      return (uint32_t)(m * e.ldo + t.n0 + 64 * wn + 16 * lg);
-    }
-  };
-  auto res_off = [&](const EpiT& t, int u, int k) __attribute__((always_inline)) {
-    return (uint32_t)(((t.r0 + 64 * wm + 16 * u + 4 * k + tb) * e.ldo + t.n0 + 64 * wn + 4 * ta) * 4);
-  };
-  // the fast path of element pairs [p0, p1) of unit u (int8-output epilogues)
-  auto epi_pairs = [&](const EpiT& t, auto U, int p0, int p1) __attribute__((always_inline)) {
-    constexpr int u = decltype(U)::value;
-    if constexpr ((NQK_PG_DIAG & 2) != 0) return;  // diagnostic: no epilogue math
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      if (p < p0 || p >= p1) continue;
-      const int q = 2 * p;
-      const v2f vf = v2f{(float)accp[u][q >> 2][q & 3], (float)accp[u][q >> 2][(q & 3) + 1]};
-      v2f dd, sv;
-      float m0, m1;
-      if constexpr (EPI == PG_QKV) {
-        const v2f uu = __builtin_elementwise_fma(vf, v2f{t.c1, t.c1}, v2f{ecol[q], ecol[q + 1]});
-        const v2f rr = v2f{__builtin_rintf(uu[0]), __builtin_rintf(uu[1])};
-        dd = uu - rr;
-        m0 = __builtin_fmaf(__builtin_fabsf(vf[0]), t.k1, __builtin_fabsf(dd[0]));
-        m1 = __builtin_fmaf(__builtin_fabsf(vf[1]), t.k1, __builtin_fabsf(dd[1]));
-        const v2f b = rr + v2f{t.zp128, t.zp128};
-        pk[q >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[0], 0.0f, 255.0f), q & 3, pk[q >> 2]);
-        pk[q >> 2] =
-            __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(b[1], 0.0f, 255.0f), (q & 3) + 1, pk[q >> 2]);
-      } else {
-        const v2f h = v2f{ecol[q], ecol[q + 1]} + vf * v2f{t.sacc, t.sacc};
-        hv[q] = h[0];
-        hv[q + 1] = h[1];
-        const v2f tf = gelu_fast2(h) * v2f{t.rsf, t.rsf};
-        sv = round_magic2(tf, t.qlo, t.qhi, t.magic, dd);
-        m0 = __builtin_fmaf(__builtin_fabsf(h[0]), e.g_rel, __builtin_fabsf(dd[0]));
-        m1 = __builtin_fmaf(__builtin_fabsf(h[1]), e.g_rel, __builtin_fabsf(dd[1]));
-      }
-      worst = __builtin_elementwise_max(worst, __builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)));
-      if constexpr (EPI != PG_QKV) {
-        if (q & 2) pk[q >> 2] = pack4_low(sprev, sv);
-        sprev = sv;
-      }
-    }
-  };
-  // end of unit u (int8 outputs): the rounding filter's exact fallback for the elements it
-  // could not decide (rare: a wave-uniform branch), bytes to two's complement, the store
-  auto epi_finish = [&](const EpiT& t, int cslot, auto U) __attribute__((always_inline)) {
-    constexpr int u = decltype(U)::value;
-    if constexpr (EPI == PG_QKV) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) pk[g] ^= 0x80808080u;
-    }
-    if (__builtin_expect(__any(worst >= __float_as_uint(t.lim)), 0) && (NQK_PG_DIAG & 32) == 0) {
-      const float s_out = t.g3 == 0 ? e.s_out[0] : (t.g3 == 1 ? e.s_out[1] : e.s_out[2]);
-      const double rs_out = t.g3 == 0 ? e.rs_out[0] : (t.g3 == 1 ? e.rs_out[1] : e.rs_out[2]);
-      const double zp = t.g3 == 0 ? e.zp_out[0] : (t.g3 == 1 ? e.zp_out[1] : e.zp_out[2]);
-      const int8_t* bp = lds + P2_COLP + cslot * 2048 + 1024 + (64 * wn + 16 * lg) * 4;
-      int av[16];
-      float xv[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        av[q] = accp[u][q >> 2][q & 3];
-        xv[q] = EPI == PG_QKV ? *reinterpret_cast<const float*>(bp + 4 * q) : hv[q];
-      }
-      pg_exact_fix<EPI>(av, xv, pk, PgFix{t.c1, t.k1, t.rsf, t.sacc, t.lim, s_out, rs_out, zp}, e);
-    }
-    const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
-    if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-    else __builtin_amdgcn_raw_buffer_store_b128(st, t.out, unit_off(t, u), 0, 0);
-  };
-  // RESID unit u: residual loads (phase 0), then (last phase) the transposed accumulators
-  // through the wave's LDS scratch, y = (bias + RN(v sacc)) + residual, whole-line stores
-  auto res_load = [&](const EpiT& t, auto U) __attribute__((always_inline)) {
-    constexpr int u = decltype(U)::value;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) resv[k] = pg_load16(t.res, res_off(t, u, k), 0u);
-  };
-  auto res_unit = [&](const EpiT& t, auto U) __attribute__((always_inline)) {
-    constexpr int u = decltype(U)::value;
-    if constexpr ((NQK_PG_DIAG & 2) != 0) {  // diagnostic: no epilogue math / LDS transpose
-      const v4u st = v4u{resv[0][0], resv[1][1], resv[2][2], resv[3][3]} ^ (v4u)accp[u][0];
-      if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-      else __builtin_amdgcn_raw_buffer_store_b128(st, t.out, res_off(t, u, 0), 0, 0);
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) *reinterpret_cast<v4i*>(tr + l15 * P2_TR_ROW + (16 * j + 4 * lg) * 4) = accp[u][j];
-    v4i tv[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) tv[k] = *reinterpret_cast<const v4i*>(tr + (4 * k + tb) * P2_TR_ROW + 16 * ta);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v4u st;
-      if constexpr (F32X) {
-        const v2f d01 = v2f{(float)tv[k][0], (float)tv[k][1]} * v2f{t.sacc, t.sacc};
-        const v2f d23 = v2f{(float)tv[k][2], (float)tv[k][3]} * v2f{t.sacc, t.sacc};
-        const v2f y01 = (v2f{ecol[0], ecol[1]} + d01) + v2f{__uint_as_float(resv[k][0]), __uint_as_float(resv[k][1])};
-        const v2f y23 = (v2f{ecol[2], ecol[3]} + d23) + v2f{__uint_as_float(resv[k][2]), __uint_as_float(resv[k][3])};
-        st = v4u{__float_as_uint(y01[0]), __float_as_uint(y01[1]), __float_as_uint(y23[0]), __float_as_uint(y23[1])};
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float d = (float)((double)tv[k][r] * (double)t.sacc);
-          st[r] = __float_as_uint((ecol[r] + d) + __uint_as_float(resv[k][r]));
-        }
-      }
-      if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
-      else __builtin_amdgcn_raw_buffer_store_b128(st, t.out, res_off(t, u, k), 0, 0);
-    }
-  };
-
-  // ------------------------------------------------------------ MFMA half steps
-  // 8 MFMAs (M-subtiles 2 h, 2 h + 1 x the 4 N-subtiles); the caller's other work of the
-  // half is in the same scheduling region, so the compiler places it between the MFMAs
-  auto mfma_half = [&](auto H, auto FIRST, const v4i (&aa)[2], const v4i (&bb)[4]) __attribute__((always_inline)) {
-    constexpr int h = decltype(H)::value;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int ii = q >> 2, j = q & 3;
-      if constexpr (decltype(FIRST)::value)
-        acc[2 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], cinit[j], 0, 0, 0);
-      else
-        acc[2 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], acc[2 * h + ii][j], 0, 0, 0);
-    }
-  };
-
-  // ------------------------------------------------------------ prologue
-  Src cur = src_of(0);
-  issue_colp(cur.tn, 0);
-  issue_stage(cur, 0, 0);
-  issue_stage(cur, 1, 1);
-  issue_stage(cur, 2, 2);
-  pg_vmcnt<2 * P2_PW>();  // stage 0 and the column constants landed (stages 1, 2 may fly)
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  sfor<0, 2>([&](auto Q) __attribute__((always_inline)) { rd_a(a01, ic<0>{}, ic<0>{}, Q); });
-  sfor<0, 4>([&](auto Q) __attribute__((always_inline)) { rd_b(b0, ic<0>{}, Q); });
-  rd_cinit(0);
-  EpiT et = epi_setup(cur, 0, false);  // no previous tile: zero-size descriptors
-
-  for (int it = 0; it < cnt; ++it) {
-    const Src nxt = src_of(it + 1);  // = cur's source for the last tile (re-staged, never read)
-    const int cs = it % 3, cs_prev = (it + 2) % 3, cs_next = (it + 1) % 3;
-    if (it > 0) et = epi_setup(src_of(it - 1), cs_prev, true);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cinit[j] = -cinit[j];
-    sfor<0, NK>([&](auto KT) __attribute__((always_inline)) {
-      constexpr int kt = decltype(KT)::value;
-      constexpr int slot = kt % P2_RD;
-      constexpr int u = S::unit(kt);
-      v4i(&bc)[4] = (kt & 1) ? b1 : b0;
-      v4i(&bn)[4] = (kt & 1) ? b0 : b1;
-      // ---- half 1: subtiles 0, 1; the A fragments of subtiles 2, 3; stage kt + 3 (this
-      // tile's, or the next tile's first three); the epilogue's first pairs of the step
-      if constexpr (EPI != PG_RESID)
-        if constexpr (S::ph(kt) == 0) {
-          worst = 0;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) pk[g] = 0;
-        }
-      mfma_half(ic<0>{}, std::integral_constant<bool, kt == 0>{}, a01, bc);
-      rd_a(a23, ic<slot>{}, ic<2>{}, ic<0>{});
-      rd_a(a23, ic<slot>{}, ic<2>{}, ic<1>{});
-      if constexpr (kt + 3 < NK) issue_stage(cur, kt + 3, (kt + 3) % P2_RD);
-      else issue_stage(nxt, kt + 3 - NK, (kt + 3) % P2_RD);
-      if constexpr (EPI != PG_RESID) epi_pairs(et, ic<u>{}, S::plo(kt, 0), S::phi(kt, 0));
-      // ---- middle: stage kt + 1 landed (exact count of younger VMEM operations; the
-      // first tile's first steps follow the prologue instead of a previous tile)
-      if constexpr (kt < 2) {
-        if (it == 0) {
-          if constexpr (kt == 0) pg_vmcnt<P2_PW + P2_PW>();
-          else pg_vmcnt<S::half2_ops(0) + P2_PW + P2_PW>();
-        } else {
-          pg_vmcnt<S::younger(kt)>();
-        }
-      } else {
-        pg_vmcnt<S::younger(kt)>();
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- half 2: subtiles 2, 3; the next step's fragments (and at the tile's end the
-      // next tile's initial accumulators); colp of the next tile (step 1); the epilogue
-      if constexpr (kt == 1) issue_colp(nxt.tn, cs_next);
-      if constexpr (EPI == PG_RESID && S::ph(kt) == 0) res_load(et, ic<u>{});
-      mfma_half(ic<1>{}, std::integral_constant<bool, kt == 0>{}, a23, bc);
-      rd_a(a01, ic<(kt + 1) % P2_RD>{}, ic<0>{}, ic<0>{});
-      rd_a(a01, ic<(kt + 1) % P2_RD>{}, ic<0>{}, ic<1>{});
-      sfor<0, 4>([&](auto Q) __attribute__((always_inline)) { rd_b(bn, ic<(kt + 1) % P2_RD>{}, Q); });
-      if constexpr (kt == NK - 1) rd_cinit(cs_next);
-      if constexpr (EPI != PG_RESID) {
-        epi_pairs(et, ic<u>{}, S::plo(kt, 1), S::phi(kt, 1));
-        if constexpr (S::last(kt)) epi_finish(et, cs_prev, ic<u>{});
-      } else {
-        if constexpr (S::last(kt)) res_unit(et, ic<u>{});
-      }
-    });
-    // tile it's results become the previous tile's
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) accp[i][j] = acc[i][j];
-    cur = nxt;
-  }
-  // the last tile's epilogue (nothing left to overlap with)
-  {
-    const int it = cnt;
-    et = epi_setup(src_of(it - 1), (it + 2) % 3, true);
-    sfor<0, 4>([&](auto U) __attribute__((always_inline)) {
-      if constexpr (EPI == PG_RESID) {
-        res_load(et, U);
-        res_unit(et, U);
-      } else {
-        worst = 0;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) pk[g] = 0;
-        epi_pairs(et, U, 0, 8);
-        epi_finish(et, (it + 2) % 3, U);
-      }
-    });
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 // weight image of k_pg: [N / 256][K / 64] stages of 256 rows x 64 B in the LDS order of the
 // stage (row rho: column 64 (rho >> 6) + pg_bperm(rho & 63) of the panel; physical chunk
@@ -1433,9 +83,10 @@ static int pg_num_cus() {
   return n;
 }
 
-// Launches k_pg2 (or k_pg) for one projection GEMM when it takes the case; returns the
-// kernel id for nqk_qgemm_last_kernel (5 k_pg2, 4 k_pg) if launched, 0 if the caller must
-// use another kernel, < 0 on error.  bp: the nqk_pack_pg image.
+// Launches k_pg for one projection GEMM when it takes the case; returns the kernel id for
+// nqk_qgemm_last_kernel (4 k_pg, 6 k_pg with the GELU table) if launched, 0 if the caller
+// must use another kernel, < 0 on error.  bp: the nqk_pack_pg image.  (Round 4's k_pg2 —
+// the epilogue inside the next tile's k loop — measured slower and was removed)
 int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, int64_t K, int64_t lda,
               const nqk_epilogue* p, bool f32x) {
   if (getenv("NQK_NO_PG")) return 0;
@@ -1460,14 +111,28 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   // NQK_PG_NORESID=1 keeps the residual epilogues on k_qgemm_big (the round-2 kernel)
   if (epi == PG_RESID && (getenv("NQK_PG_NORESID") || p->resid == nullptr || (M % PG_BM != 0 && p->resid == p->out[0])))
     return 0;
+  // WM = 2: 256 x 256 tiles, one 512-thread workgroup per CU, B shared by the two row halves
+  // (NQK_PG_WM=1 / 2 forces one form where both exist)
+  int wm = 1;
+  {
+    const char* wv = getenv("NQK_PG_WM");
+    if (wv) wm = atoi(wv) == 2 ? 2 : 1;
+    if (wm == 2 && (K == 192 || M < 2 * PG_BM || (epi == PG_RESID && M % (2 * PG_BM) != 0 && p->resid == p->out[0])))
+      wm = 1;
+  }
   if (epi == PG_GELU && !(p->div == 1.41421354f && p->add1 == 1.0f && p->mul2 == 0.5f)) return 0;
   auto al16 = [](const void* q) { return q == nullptr || (((uintptr_t)q) & 15) == 0; };
   if (!al16(p->out[0]) || !al16(p->out[1]) || !al16(p->out[2]) || !al16(p->resid) || !al16(p->colterm) ||
       !al16(p->bias) || !al16(a) || (lda & 15))
     return 0;
   // GELU with a table (nqk_gelu_lut_build): the table holds the exact chain's output bytes
-  const bool glut = epi == PG_GELU && p->gelu_lut != nullptr && p->lut_n > 0 && p->lut_n <= GLUT_MAX &&
-                    (((uintptr_t)p->gelu_lut) & 15) == 0 && !getenv("NQK_NO_GLUT");
+  // (a table of more than GLUT_CAP1 entries needs the 256 x 256-tile form's LDS: ViT-Ti's FFN-up)
+  bool glut = epi == PG_GELU && p->gelu_lut != nullptr && p->lut_n > 0 && p->lut_n <= GLUT_MAX &&
+              (((uintptr_t)p->gelu_lut) & 15) == 0 && !getenv("NQK_NO_GLUT");
+  if (glut && p->lut_n > GLUT_CAP1) {
+    if (M >= 2 * PG_BM && !b4 && f32x && (K == 192 || K == 768)) wm = 2;
+    else glut = false;
+  }
   if (p->bit_width < 2 || p->bit_width > 8) return 0;  // int8 outputs
   const double qlo = -__builtin_ldexp(1.0, p->bit_width - 1), qhi = __builtin_ldexp(1.0, p->bit_width - 1) - 1.0;
   PgEpi e{};
@@ -1518,76 +183,22 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     const float g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
     e.g_lim = (float)((0.5 - (double)g_abs) * (1.0 - 0x1p-22));
   }
-  const int tiles_n = (int)((N + PG_BN - 1) / PG_BN), tiles_m = (int)((M + PG_BM - 1) / PG_BM);
+  const int tiles_n = (int)((N + PG_BN - 1) / PG_BN), tiles_m = (int)((M + wm * PG_BM - 1) / (wm * PG_BM));
   const int nt = tiles_m * tiles_n;
-  // k_pg (two workgroups per CU, epilogue after the k loop) by default; NQK_PG_KERNEL=2
-  // selects k_pg2 (epilogue inside the next tile's k loop, one workgroup per CU), measured
-  // slower (its interleaved epilogue does not hide behind the MFMAs)
-  const char* kv = getenv("NQK_PG_KERNEL");
-  if (kv && atoi(kv) == 2 && K != 192 && N % PG_BN == 0 && !b4 && p->bit_width == 8) {
-    const int grid2 = nt < pg_num_cus() ? nt : pg_num_cus();
-    const int key2 = epi * 4 + (K == 3072 ? 2 : 0) + (f32x ? 1 : 0);
-    switch (key2) {
-#define PG2L(E, NKV, X)                                                                                           \
-  case E * 4 + (NKV == 48 ? 2 : 0) + (X ? 1 : 0):                                                                 \
-    hipLaunchKernelGGL((k_pg2<E, NKV, X>), dim3(grid2), dim3(512), p2_lds(E), stream(), a, bp, (int)M, (int)N,    \
-                       (int)lda, tiles_n, nt, e);                                                                 \
-    break;
-      PG2L(PG_QKV, 12, true)
-      PG2L(PG_GELU, 12, true)
-      PG2L(PG_RESID, 12, true) PG2L(PG_RESID, 12, false) PG2L(PG_RESID, 48, true) PG2L(PG_RESID, 48, false)
-#undef PG2L
-      default:
-        return 0;
-    }
-    const int rc2 = launch_status("nqk_qgemm_fused(pg2)");
-    return rc2 < 0 ? rc2 : 5;
-  }
-  const int slots = 2 * pg_num_cus();
+  const int slots = (wm == 2 ? 1 : 2) * pg_num_cus();
   const int kc = K == 3072 ? 2 : (K == 192 ? 1 : 0);
   const int epi_k = glut ? PG_GLUT : epi;
   const bool s8 = epi == PG_QKV && p->bit_width == 8 && !b4 && !getenv("NQK_PG_NOS8");
-  const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0) + (s8 ? 256 : 0);
-  auto launch = [&](const int8_t* a_, int m_, int ntiles_, int grid_, const PgEpi& e_) {
-    switch (key) {
-#define PGL(E, NKV, X, B)                                                                                      \
-  case E * 16 + (NKV == 48 ? 2 : (NKV == 3 ? 1 : 0)) * 4 + (X ? 1 : 0) + (B ? 2 : 0):                          \
-    hipLaunchKernelGGL((k_pg<E, NKV, X, B>), dim3(grid_), dim3(256), pg_lds_bytes(E, B), stream(), a_, bp, m_,  \
-                       (int)N, (int)lda, tiles_n, ntiles_, e_);                                                \
-    return true;
-      case 256 + PG_QKV * 16 + 0 * 4 + 1:  // QKV, 8-bit outputs: the saturating convert clamps
-        hipLaunchKernelGGL((k_pg<PG_QKV, 12, true, false, true>), dim3(grid_), dim3(256), pg_lds_bytes(PG_QKV, false),
-                           stream(), a_, bp, m_, (int)N, (int)lda, tiles_n, ntiles_, e_);
-        return true;
-      case 256 + PG_QKV * 16 + 1 * 4 + 1:
-        hipLaunchKernelGGL((k_pg<PG_QKV, 3, true, false, true>), dim3(grid_), dim3(256), pg_lds_bytes(PG_QKV, false),
-                           stream(), a_, bp, m_, (int)N, (int)lda, tiles_n, ntiles_, e_);
-        return true;
-      PGL(PG_QKV, 12, true, false)
-      PGL(PG_GELU, 12, true, false)
-      PGL(PG_GLUT, 12, true, false)
-      PGL(PG_RESID, 12, true, false) PGL(PG_RESID, 12, false, false) PGL(PG_RESID, 48, true, false)
-      PGL(PG_RESID, 48, false, false)
-      PGL(PG_QKV, 3, true, false)  // K = 192 (ViT-Ti)
-      PGL(PG_GELU, 3, true, false)
-      PGL(PG_GLUT, 3, true, false)
-      PGL(PG_RESID, 3, true, false) PGL(PG_RESID, 3, false, false)
-      PGL(PG_QKV, 12, true, true)  // int4 weights (BASELINE configs[4])
-      PGL(PG_GELU, 12, true, true)
-      PGL(PG_GLUT, 12, true, true)
-      PGL(PG_RESID, 12, true, true) PGL(PG_RESID, 12, false, true) PGL(PG_RESID, 48, true, true)
-      PGL(PG_RESID, 48, false, true)
-#undef PGL
-      default:
-        return false;
-    }
-  };
+  const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0) + (s8 ? 256 : 0) + (wm == 2 ? 512 : 0);
+  const PgArgs x{a, bp, (int)M, (int)N, (int)lda, tiles_n, nt, nt < slots ? nt : slots, &e};
   // (A tail split — the rows of the whole rounds in one launch, the last round's row panels
   // in a second launch with one workgroup per tile — measured slower: FFN-down 142 -> 176 us,
   // out-proj 77 -> 90 us, profiles/r04_pg_split_dropped.txt)
-  if (!launch(a, (int)M, nt, nt < slots ? nt : slots, e)) return 0;
+  if (!(pg_dispatch_i8(key, x) || pg_dispatch_resid(key, x) || pg_dispatch_tiny(key, x) || pg_dispatch_i4(key, x) ||
+        pg_dispatch_wm2(key, x)))
+    return 0;
   const int rc = launch_status("nqk_qgemm_fused(pg)");
-  return rc < 0 ? rc : (glut ? 6 : 4);
+  return rc < 0 ? rc : (glut ? (wm == 2 ? 7 : 6) : (wm == 2 ? 5 : 4));
 }
 
 }  // namespace nqk

@@ -67,6 +67,11 @@ class Streams:
             _lib.call("nqk_stream_join")
             self.forked = False
 
+    def max_part(self, n: int) -> int:
+        """The most images one `halves` call hands fn (the first part's)."""
+        p = min(self.parts, n)
+        return n if (not self.enabled or p < 2) else -(-n // p)
+
     def halves(self, n: int, fn):
         """fn(stream_index, first_image, images) for the parts of n images on their
         streams (or once, whole batch on stream 0, when splitting is off / n < 2); the
@@ -89,6 +94,13 @@ class Streams:
 
 
 _ONE_STREAM = Streams(False)
+
+
+def embed_q_fits(images: int, hw: int, kout: int) -> bool:
+    """Whether one nqk_embed_q call over `images` images of hw patches takes the shape: at most
+    65535 row tiles of 128 patches, and (images x (hw + 1)) x kout < 2^31 (its 32-bit output
+    offsets; nqk_gemm.hip checks the same and refuses larger calls)."""
+    return -(-(images * hw) // 128) <= 65535 and images * (hw + 1) * kout < 2147483647
 
 
 class NoMatch(Exception):
@@ -447,8 +459,9 @@ class FusedEmbed:
             raise ValueError(f"class-token Expand shape {eshape} does not match the batch {n}")
         out = DeviceArray((n, hw + 1, self.kout), np.float32)
         # (fused_in: the zero point within nqk_patchify_dequant's / nqk_embed_q's 2^20;
-        # nqk_embed_q: at most 65535 row tiles of 128 patches, else the patchify path)
-        folded = fused_in and self.wt is not None and c == 3 and -(-(n * hw) // 128) <= 65535
+        # nqk_embed_q, per call (one per stream part): at most 65535 row tiles of 128 patches and
+        # (images x (patches + 1)) x kout < 2^31 (its 32-bit output offsets), else the patchify path)
+        folded = fused_in and self.wt is not None and c == 3 and embed_q_fits(streams.max_part(n), hw, self.kout)
         if folded:
             cols = None  # nqk_embed_q reads the int8 image itself
         elif fused_in:
@@ -784,7 +797,7 @@ def _gelu_lut(p, bit_width, div, add1, mul2):
     the filtered chain) or NQK_NO_GLUT is set."""
     if os.environ.get("NQK_NO_GLUT") or p.zero_point is None or not hasattr(_lib.load(), "nqk_gelu_lut_build"):
         return None
-    lut = DeviceArray((4096,), np.uint8)
+    lut = DeviceArray((8192,), np.uint8)
     k = (ctypes.c_float * 5)()
     n = ctypes.c_int32(0)
     _lib.call("nqk_gelu_lut_build", _f32(p.scale), int(p.zero_point), int(bit_width), _f32(div), _f32(add1),
@@ -850,7 +863,14 @@ def _gemm(epi, a, bt, batch, M, N, K, lda, ldb, bmap, a_ms, b_ms, e):
     _lib.call("nqk_qgemm_fused", epi, a.vp, bt.vp, batch, M, N, K, lda, ldb,
               _lib.i64arr(bmap) if bmap is not None else None, a_ms, b_ms, ctypes.byref(e))
     if t0 is not None:
-        KM.TIMER.end("qgemm_" + _EPI_NAMES[epi], t0, (2 * batch * M * N * K, batch * (M * K + N * K)))
+        # algorithmic HBM bytes: A, the weights, the epilogue's outputs (int8; the residual
+        # epilogues read and write f32 rows); residual GEMMs split into the attention output
+        # projection (K = N) and FFN-down (K > N)
+        name = _EPI_NAMES[epi]
+        out_b = 8 * M * N if epi == EPI_RESID else (M * N if epi in (EPI_QKV, EPI_GELU) else 0)
+        if epi == EPI_RESID:
+            name = "down" if K > N else "out"
+        KM.TIMER.end("qgemm_" + name, t0, (2 * batch * M * N * K, batch * (M * K + N * K + out_b)))
 
 
 class Workspace:
@@ -880,9 +900,8 @@ class Workspace:
         return self.bufs
 
 
-class FusedAwayError(AttributeError, RuntimeError):
-    """Reading a FusedAway value.  An AttributeError, so getattr(v, attr, default) and
-    hasattr() probes see a missing attribute instead of an exception."""
+class FusedAwayError(RuntimeError):
+    """Reading a FusedAway value."""
 
 
 class FusedAway:
@@ -893,9 +912,19 @@ class FusedAway:
     def __init__(self, name):
         self.name = name
 
+    def _error(self):
+        return FusedAwayError(f"value {self.name!r} was computed inside a fused plan step and not kept; "
+                              "set QModel.keep_values = True to read intermediates")
+
     def __getattr__(self, attr):
-        raise FusedAwayError(f"value {self.name!r} was computed inside a fused plan step and not kept; "
-                             "set QModel.keep_values = True to read intermediates")
+        if attr.startswith("__") and attr.endswith("__"):
+            # protocol probes (copy, pickle, NumPy's __array_interface__ / __array_struct__) see a
+            # missing attribute; NumPy then calls __array__, which raises
+            raise AttributeError(attr)
+        raise self._error()
+
+    def __array__(self, *args, **kwargs):
+        raise self._error()
 
     def __repr__(self):
         return f"FusedAway({self.name!r})"

@@ -38,7 +38,7 @@ def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, ker
     for k in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_NO_PG", "NQK_PG_NORESID"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("NQK_NO_PROJ", "1")
-    monkeypatch.setenv("NQK_PG_KERNEL", str(kernel))
+    monkeypatch.setenv("NQK_PG_WM", str(kernel))
     if no_f32x:
         monkeypatch.setenv("NQK_NO_F32X", "1")
     e = _lib.Epilogue()
@@ -107,15 +107,18 @@ def _numpy_ref(epi_name, M, N, K, host):
     ("resid", 256 * 197, 768, 3072, 1.0, False),
     # ragged last tile rows with more tiles than workgroup slots
     ("gelu", 128 * 50 + 77, 3072, 768, 1.0, False), ("resid", 128 * 200 + 50, 768, 768, 1.0, False),
+    ("qkv", 128 * 197 + 64, 2304, 768, 1.0, False), ("resid", 256 * 97 + 128, 768, 3072, 1.0, False),
 ])
 @pytest.mark.parametrize("kernel", [1, 2])
 def test_pg_gemm_equals_big_tile(epi_name, M, N, K, s_out_scale, no_f32x, kernel, monkeypatch):
-    """kernel 1: k_pg (two workgroups per CU); 2: k_pg2 (the epilogue of each tile inside
-    the next tile's k loop)."""
+    """kernel 1: k_pg on 128 x 256 tiles (two 256-thread workgroups per CU); 2: k_pg on
+    256 x 256 tiles (NQK_PG_WM=2: one 512-thread workgroup per CU, both row halves reading the
+    same B stage; below 256 rows, or ragged in place, the launcher keeps the 128-row form)."""
     seed = M + N + K
     k0, ref, host = _run(epi_name, M, N, K, s_out_scale, False, no_f32x, monkeypatch, seed, kernel)
     k1, got, _ = _run(epi_name, M, N, K, s_out_scale, True, no_f32x, monkeypatch, seed, kernel)
-    assert (k0, k1) == (1, 3 + kernel), (k0, k1)
+    wm2 = kernel == 2 and M >= 256
+    assert (k0, k1) == (1, 5 if wm2 else 4), (k0, k1)
     if M <= 1024:
         npref = _numpy_ref(epi_name, M, N, K, host)
         if npref is not None:

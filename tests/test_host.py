@@ -272,3 +272,31 @@ def test_redimension_vit_base_to_tiny():
         np.testing.assert_array_equal(onnx_proto.to_array(t), a[t.name])
     with pytest.raises(ValueError):
         onnx_proto.redimension(onnx_proto.load(path, synthetic_weights=True), 192, 4, 768)
+
+
+def test_embed_fold_guard_per_stream_part():
+    """nqk_embed_q's 32-bit output offsets need (images x 197) x 768 < 2^31 per call
+    (one call per stream part); past that the plan keeps the patchify path instead of failing."""
+    from numpy_quant.plan import Streams, embed_q_fits
+    two, one = Streams(True, 2), Streams(False)
+    assert two.max_part(256) == 128 and two.max_part(257) == 129 and one.max_part(257) == 257
+    assert embed_q_fits(two.max_part(256), 196, 768)
+    assert embed_q_fits(14_000, 196, 768) and not embed_q_fits(14_200, 196, 768)
+    assert embed_q_fits(two.max_part(28_000), 196, 768)       # 14 000 per part
+    assert not embed_q_fits(two.max_part(28_500), 196, 768)   # 14 250 per part: past 2^31
+    assert not embed_q_fits(one.max_part(20_000), 196, 768)   # one stream: the whole batch in one call
+    assert not embed_q_fits(45_000, 196, 64)                  # 65535 row tiles
+
+
+def test_fused_away_value_raises_on_read():
+    """reading a value that a fused step never materialised raises a RuntimeError
+    (FusedAwayError), also through NumPy's array conversion; protocol probes see a missing
+    attribute."""
+    from numpy_quant.plan import FusedAway, FusedAwayError
+    v = FusedAway("x")
+    with pytest.raises(FusedAwayError):
+        v.data
+    with pytest.raises(FusedAwayError):
+        np.asarray(v)
+    assert not isinstance(FusedAwayError("m"), AttributeError)
+    assert getattr(v, "__array_interface__", None) is None

@@ -40,6 +40,30 @@ def test_launcher_spawns_world2_ranks():
         assert d["master"] == "127.0.0.1" and d["header_from"] == 0 and d["max_rank"] == 1.0
 
 
+def test_dead_rank_fails_the_launch_fast():
+    """A rank that exits non-zero before the rendezvous leaves rank 0 waiting on the control
+    plane (600 s) — or, past the rendezvous, inside an RCCL collective; the parent must notice
+    the dead rank, stop the others and exit with its status within seconds."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["NQK_DRY_RUN_EXIT_RANK"] = "1"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    dt = time.monotonic() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert dt < 30, dt
+    assert "rank 1 exited with status 3" in r.stderr
+
+
+def test_spawn_ranks_deadline(tmp_path):
+    """Every rank still running past the launcher's deadline is stopped: status 124."""
+    script = tmp_path / "sleeper.py"
+    script.write_text("import time\ntime.sleep(60)\n")
+    rc = bench.spawn_ranks(2, [], timeout=1.0, script=str(script))
+    assert rc == 124
+
+
 def test_world_size_mismatch_is_refused():
     env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],

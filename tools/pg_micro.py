@@ -83,7 +83,7 @@ def setup(name):
     e.b_packed = kind
     glut = None
     if epi == 4:  # the GELU table of these output parameters (round 4: the "glut" variant)
-        lut = DeviceArray((4096,), np.uint8)
+        lut = DeviceArray((8192,), np.uint8)
         kk = (ctypes.c_float * 5)()
         nn = ctypes.c_int32(0)
         _lib.call("nqk_gelu_lut_build", e.s_out[0], e.zp_out[0], 8, e.div, e.add1, e.mul2, lut.vp, kk, ctypes.byref(nn))
@@ -137,7 +137,9 @@ for name in sel:
     if keep[-1] is not None:
         for lname, lib in libs.items():
             variants.append(("glut" if lname == "main" else f"glut:{lname}", lib, {}, "glut"))
-    variants.append(("pg2", main, {"NQK_PG_KERNEL": "2"}, True))
+    variants.append(("pg:wm2", main, {"NQK_PG_WM": "2"}, True))
+    if keep[-1] is not None:
+        variants.append(("glut:wm2", main, {"NQK_PG_WM": "2"}, "glut"))
     variants.append(("r02", main, {"NQK_PROJ_GELU": "1"} if epi == 4 else {}, False))
     res = {v[0]: [] for v in variants}
     for _ in range(ROUNDS):
