@@ -209,7 +209,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     }
 #endif
   }
-  __syncthreads();
+  if constexpr ((NQK_ATTN_DIAG & 1024) == 0) __syncthreads();  // (diagnostic 1024: no workgroup barriers)
   for (int row = tid; row < TP; row += 256) {
     const v4i* kr = reinterpret_cast<const v4i*>(Ks + row * 64);
     colK[row] = (sum16a(kr[0]) + sum16a(kr[1]) + sum16a(kr[2]) + sum16a(kr[3])) * a.zq - a.kq;
@@ -222,7 +222,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     s += __shfl_xor(s, 2, 64);
     if (part == 0) colV[d] = s * a.zp - a.kp;
   }
-  __syncthreads();
+  if constexpr ((NQK_ATTN_DIAG & 1024) == 0) __syncthreads();
 
   // pairwise-sum plan of a row (uniform): leaf l = [s0_l, s0_l + L_l), main part of
   // ng_l whole 8-groups from group g0_l, then a tail of tl_l < 8 columns
@@ -243,8 +243,13 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
       // (Q rows by LDS-DMA at the workgroup's start instead: no faster on the bench's data,
       // profiles/r04_attn_real_data.txt)
       const int qrow = min(m, T - 1);
-      qb[0] = *reinterpret_cast<const v4i*>(q + qrow * 64 + h * 16);
-      qb[1] = *reinterpret_cast<const v4i*>(q + qrow * 64 + (2 + h) * 16);
+      if constexpr ((NQK_ATTN_DIAG & 2048) != 0) {  // (diagnostic 2048: Q rows from the LDS K image, no Q loads)
+        qb[0] = *reinterpret_cast<const v4i*>(Ks + swz64a(qrow, h));
+        qb[1] = *reinterpret_cast<const v4i*>(Ks + swz64a(qrow, 2 + h));
+      } else {
+        qb[0] = *reinterpret_cast<const v4i*>(q + qrow * 64 + h * 16);
+        qb[1] = *reinterpret_cast<const v4i*>(q + qrow * 64 + (2 + h) * 16);
+      }
     }
     int rq = sum16a(qb[0]) + sum16a(qb[1]);
     rq += xor32i(rq);

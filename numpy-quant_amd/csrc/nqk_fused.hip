@@ -1600,6 +1600,9 @@ k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const f
 // quantize chain, 40.9 vs 39.3 us per launch at 50432 x 768, profiles/r04_ln_filter_dropped.txt;
 // two row groups per wave with the second group's loads under the first's work, 40.8 vs
 // 39.7 us, profiles/r04_ln_gpw_dropped.txt.)
+#ifndef NQK_LN_NT
+#define NQK_LN_NT 0  // 1: the f32 row loads non-temporal (read once; A/B variant, round 5)
+#endif
 template <int NL>
 __global__ void __launch_bounds__(256)
 k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
@@ -1623,7 +1626,13 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
   for (int k = 0; k < NLD; ++k) {
     const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
     const int64_t gr = row0 + r < rows ? row0 + r : rows - 1;
-    ld[k] = *reinterpret_cast<const float4*>(x + gr * COLS + c * 4);
+    if constexpr (NQK_LN_NT) {
+      typedef float v4f_nt __attribute__((ext_vector_type(4)));
+      const v4f_nt v = __builtin_nontemporal_load(reinterpret_cast<const v4f_nt*>(x + gr * COLS + c * 4));
+      ld[k] = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      ld[k] = *reinterpret_cast<const float4*>(x + gr * COLS + c * 4);
+    }
   }
 #pragma unroll
   for (int k = 0; k < NLD; ++k) {

@@ -189,7 +189,11 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   const int kc = K == 3072 ? 2 : (K == 192 ? 1 : 0);
   const int epi_k = glut ? PG_GLUT : epi;
   const bool s8 = epi == PG_QKV && p->bit_width == 8 && !b4 && !getenv("NQK_PG_NOS8");
-  const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0) + (s8 ? 256 : 0) + (wm == 2 ? 512 : 0);
+  // K = 192 (three k steps): NQK_PG_RB=1 keeps the weight panel resident (RB; measured no faster
+  // at the ViT-Ti shapes: QKV 23.4 vs 23.4 us, GELU table 34.6 vs 34.9, profiles/r05_tiny_rb_embed_ab.txt)
+  const char* rbv = getenv("NQK_PG_RB");
+  const bool rb = K == 192 && !b4 && epi != PG_RESID && rbv && atoi(rbv) != 0;
+  const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0) + (s8 ? 256 : 0) + (wm == 2 ? 512 : 0) + (rb ? 1024 : 0);
   const PgArgs x{a, bp, (int)M, (int)N, (int)lda, tiles_n, nt, nt < slots ? nt : slots, &e};
   // (A tail split — the rows of the whole rounds in one launch, the last round's row panels
   // in a second launch with one workgroup per tile — measured slower: FFN-down 142 -> 176 us,

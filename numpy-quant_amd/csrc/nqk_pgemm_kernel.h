@@ -367,12 +367,18 @@ constexpr float PG_QLIM = 0x1.fffffcp-2f;
 // S8 (QKV with 8-bit outputs): v_cvt_pk_u8_f32 saturates to [0, 255] (tools/micro/cvtu8.hip:
 // every integral f32 in [-2^24, 2^24], profiles/r04_cvtu8.txt), which is then the clamp, so the
 // v_med3 before it goes.
-template <int EPI, int NK, bool F32X, bool B4, bool S8 = false, int WM = 1>
+// RB (round 5, K = 192 = three k steps: ViT-Ti): the whole K of a tile fits the ring, so the
+// weight panel stays RESIDENT — tiles are numbered column-panel major, a workgroup reloads B only
+// when its next tile is in another panel, and streams only A (24 KiB -> 8 KiB of operand bytes
+// per tile: one third); the k loop runs without loads or barriers, the next tile's A is issued
+// right after it, under the epilogue.
+template <int EPI, int NK, bool F32X, bool B4, bool S8 = false, int WM = 1, bool RB = false>
 __global__ void __launch_bounds__(256 * WM, 2 / WM)
 k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
      PgEpi e) {
   static_assert(NK % PG_RD == 0 && (NK >= 2 * PG_RD || NK == PG_RD), "k_pg: NK a multiple of the ring depth");
   static_assert(WM == 1 || WM == 2, "k_pg: one or two 128-row halves per tile");
+  static_assert(!RB || (NK == PG_RD && !B4 && EPI != PG_RESID), "k_pg<RB>: K = 3 k steps, int8, not residual");
   constexpr bool RESID = EPI == PG_RESID;
   constexpr int BM = PG_BM * WM;                // tile rows
   constexpr int ASTG = PG_ASTG * WM;            // A bytes of a stage
@@ -411,8 +417,15 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   struct Src { uint32_t sa, sb; int r0, tn; };
   auto src_of = [&](int tile) __attribute__((always_inline)) {
     Src s;
-    const int tm = tile / tiles_n;
-    s.tn = tile - tm * tiles_n;
+    int tm;
+    if constexpr (RB) {  // column-panel major: consecutive tiles share their weight panel
+      const int tms = ntiles / tiles_n;
+      s.tn = tile / tms;
+      tm = tile - s.tn * tms;
+    } else {
+      tm = tile / tiles_n;
+      s.tn = tile - tm * tiles_n;
+    }
     // a ragged last tile row is computed as rows M - BM .. M - 1 (the rows it shares
     // with the tile above are written twice with the same values; host: out != resid)
     s.r0 = tm * BM < M - BM ? tm * BM : M - BM;
@@ -813,6 +826,82 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   constexpr int EOPS = RESID ? 32 : 8;
   constexpr int PWA = PW;
   Src cur = src_of(tile_at(0));
+  if constexpr (RB) {
+    // VMEM operations per wave, in issue order: [B pieces when the panel changes], colp(next),
+    // the next tile's A pieces (3 k steps), then the epilogue's EOPS stores: waiting for all but
+    // EOPS waits for everything the next tile reads
+    if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
+    auto issue_b = [&](const Src& s) __attribute__((always_inline)) {
+#pragma unroll
+      for (int kt = 0; kt < NK; ++kt)
+#pragma unroll
+        for (int p = 2; p < PW; ++p) issue_piece(s, kt, kt, p);
+    };
+    auto issue_a = [&](const Src& s) __attribute__((always_inline)) {
+#pragma unroll
+      for (int kt = 0; kt < NK; ++kt)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) issue_piece(s, kt, kt, p);
+    };
+    int ctn = cur.tn;
+    issue_b(cur);
+    issue_colp(cur.tn, 0);
+    issue_a(cur);
+    for (int it = 0; it < iters; ++it) {
+      if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(0);
+      const bool more = it + 1 < iters;
+      const Src nxt = src_of(tile_at(more ? it + 1 : it));
+      const int cs = it & 1;
+      if (it == 0) pg_vmcnt<0>();
+      else pg_vmcnt<EOPS>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      v4i cinit[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cinit[j] = pg_lds16(lds + COLP + cs * 2048 + (64 * wn + 16 * lg + 4 * j) * 4);
+      sfor<0, 4>([&](auto Q) __attribute__((always_inline)) {
+        rd_a(a_lo, ic<0>{}, ic<0>{}, Q);
+        rd_b(b0, ic<0>{}, Q);
+      });
+      pg_lgkm_tie8(a_lo, b0);
+      pg_lgkm_tie(cinit[0], cinit[1], cinit[2], cinit[3]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cinit[j] = -cinit[j];
+      sfor<0, NK>([&](auto KT) __attribute__((always_inline)) {
+        constexpr int kt = decltype(KT)::value;
+        v4i(&bc)[4] = (kt & 1) ? b1 : b0;
+        v4i(&bn)[4] = (kt & 1) ? b0 : b1;
+        if constexpr (kt > 0) pg_lgkm_tie8(a_lo, bc);
+        half(ic<0>{}, std::integral_constant<bool, kt == 0>{}, a_lo, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
+          constexpr int q = decltype(Q)::value;
+          if constexpr (q < 4) rd_a(a_hi, ic<kt>{}, ic<4>{}, Q);
+        });
+        pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
+        half(ic<1>{}, std::integral_constant<bool, kt == 0>{}, a_hi, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
+          constexpr int q = decltype(Q)::value;
+          if constexpr (kt + 1 < NK) {
+            if constexpr (q < 4) rd_a(a_lo, ic<kt + 1>{}, ic<0>{}, Q);
+            else if constexpr (q < 8) rd_b(bn, ic<kt + 1>{}, ic<q - 4>{});
+          }
+        });
+      });
+      // every wave is done reading this tile's A (and B, if the panel changes)
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (nxt.tn != ctn) {  // (wave-uniform; rare: a workgroup's tiles are mostly one panel)
+        issue_b(nxt);
+        ctn = nxt.tn;
+      }
+      issue_colp(nxt.tn, cs ^ 1);
+      issue_a(nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(1);
+      epilogue(cur, cs);
+      cur = nxt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
   // PG_GLUT: the 4 KiB GELU table into LDS, 1 KiB per wave (waited for with stage 0)
   // (WM = 2: the 8 KiB of a table of up to GLUT_MAX entries, 1 KiB per wave as well)
   if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
@@ -954,15 +1043,16 @@ bool pg_dispatch_tiny(int key, const PgArgs& x);
 bool pg_dispatch_i4(int key, const PgArgs& x);
 bool pg_dispatch_wm2(int key, const PgArgs& x);
 
-// launch keys: EPI * 16 + (K 3072: 2, K 192: 1, else 0) * 4 + F32X + 2 B4 + 256 S8 + 512 WM2
-constexpr int pg_key(int epi, int nk, bool f32x, bool b4, bool s8, int wm) {
+// launch keys: EPI * 16 + (K 3072: 2, K 192: 1, else 0) * 4 + F32X + 2 B4 + 256 S8 + 512 WM2 + 1024 RB
+constexpr int pg_key(int epi, int nk, bool f32x, bool b4, bool s8, int wm, bool rb = false) {
   return epi * 16 + (nk == 48 ? 2 : (nk == 3 ? 1 : 0)) * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0) + (s8 ? 256 : 0) +
-         (wm == 2 ? 512 : 0);
+         (wm == 2 ? 512 : 0) + (rb ? 1024 : 0);
 }
-#define NQK_PG_CASE(E, NKV, X, B, S, W)                                                                        \
-  case pg_key(E, NKV, X, B, S, W):                                                                             \
-    hipLaunchKernelGGL((k_pg<E, NKV, X, B, S, W>), dim3(x.grid), dim3(256 * W), pg_lds_bytes(E, B, W), stream(), \
+#define NQK_PG_CASE_RB(E, NKV, X, B, S, W, R)                                                                  \
+  case pg_key(E, NKV, X, B, S, W, R):                                                                          \
+    hipLaunchKernelGGL((k_pg<E, NKV, X, B, S, W, R>), dim3(x.grid), dim3(256 * W), pg_lds_bytes(E, B, W), stream(), \
                        x.a, x.bp, x.m, x.n, x.lda, x.tiles_n, x.ntiles, *static_cast<const PgEpi*>(x.epi));    \
     return true;
+#define NQK_PG_CASE(E, NKV, X, B, S, W) NQK_PG_CASE_RB(E, NKV, X, B, S, W, false)
 
 }  // namespace nqk

@@ -82,19 +82,19 @@ def test_gelu_table_refuses_other_chains():
     assert n.value == 0
 
 
-def _gelu_gemm(M, N, K, s_out, zp, seed, table, monkeypatch, wm=0):
+def _gelu_gemm(M, N, K, s_out, zp, seed, table, monkeypatch, wm=0, wbits=8):
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray
     from numpy_quant.plan import EPI_GELU, _gemm, _pack_b, _pack_pg
     rng = np.random.default_rng(seed)
     a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
-    bt_h = rng.integers(-24, 25, size=(N, K), dtype=np.int8)
+    bt_h = rng.integers(-24, 25, size=(N, K), dtype=np.int8) if wbits == 8 else rng.integers(-8, 8, size=(N, K), dtype=np.int8)
     bt = DeviceArray.from_host(bt_h)
     col_h = bt_h.astype(np.int64).sum(axis=1)
     col = DeviceArray.from_host(col_h)
     bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
-    packed, kind = _pack_b(bt, 8)
-    pg = _pack_pg(bt, 8, 0)
+    packed, kind = _pack_b(bt, wbits)
+    pg = _pack_pg(bt, wbits, 0, nibbles=kind == 2)
     zpa = -5
     colterm = DeviceArray.from_host((col_h * zpa).astype(np.int32))
     for v in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_NO_PG", "NQK_NO_GLUT", "NQK_PG_WM"):
@@ -102,7 +102,8 @@ def _gelu_gemm(M, N, K, s_out, zp, seed, table, monkeypatch, wm=0):
     if wm:
         monkeypatch.setenv("NQK_PG_WM", str(wm))
     e = _lib.Epilogue()
-    e.zp_flags, e.bit_width = _lib.ZP_COL, 8
+    obits = 8 if wbits == 8 else 4  # int4 weights come with 4-bit outputs (the int4 model)
+    e.zp_flags, e.bit_width = _lib.ZP_COL, obits
     e.zpa, e.col, e.col_absmax = zpa, col.ptr, int(np.abs(col_h).max())
     e.bias, e.b_packed, e.colterm, e.bt_pg = bias.ptr, kind, colterm.ptr, pg.ptr
     e.group_cols = 1 << 30
@@ -112,7 +113,7 @@ def _gelu_gemm(M, N, K, s_out, zp, seed, table, monkeypatch, wm=0):
     e.div, e.add1, e.mul2 = SQRT2_F32, 1.0, 0.5
     keep = None
     if table:
-        lut, k, n = _build(s_out, zp)
+        lut, k, n = _build(s_out, zp, obits)
         assert n > 0
         e.gelu_lut, e.lut_n = lut.ptr, n
         for j in range(5):
@@ -138,4 +139,15 @@ def test_pg_gelu_table_equals_filtered_chain(M, N, K, s_out, zp, wm, monkeypatch
     two = wm == 2 and K != 192 and M >= 256
     big = _build(s_out, zp)[2] > 512
     assert (k0, k1) == (5 if two else 4, 7 if (two or big) else 6), (k0, k1)
+    np.testing.assert_array_equal(ref, got)
+
+
+@pytest.mark.parametrize("M", [128 * 197, 300])
+def test_pg_gelu_table_int4_weights(M, monkeypatch):
+    """the table epilogue on nibble-packed int4 weights (k_pg<PG_GLUT, B4>, the int4
+    B = 256 forward's FFN-up) equals the filtered chain on the same weights, bit for bit."""
+    s_out, zp = 0.05, 3  # 4-bit outputs (the table of CASES' (0.05, 3, 4))
+    k0, ref = _gelu_gemm(M, 3072, 768, s_out, zp, M + 4, False, monkeypatch, wbits=4)
+    k1, got = _gelu_gemm(M, 3072, 768, s_out, zp, M + 4, True, monkeypatch, wbits=4)
+    assert (k0, k1) == (4, 6), (k0, k1)
     np.testing.assert_array_equal(ref, got)

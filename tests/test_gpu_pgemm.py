@@ -17,14 +17,15 @@ def _last_kernel():
     return _lib.load().nqk_qgemm_last_kernel()
 
 
-def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, kernel=2, bw=8, l1=False):
+def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, kernel=2, bw=8, l1=False, proj=False):
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray
     from numpy_quant.plan import EPI_GELU, EPI_QKV, EPI_RESID, _gemm, _pack_b, _pack_pg
     epi = {"qkv": EPI_QKV, "resid": EPI_RESID, "gelu": EPI_GELU}[epi_name]
     rng = np.random.default_rng(seed)
     a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
-    bt_h = rng.integers(-24, 25, size=(N, K), dtype=np.int8) if bw == 8 else rng.integers(-8, 8, size=(N, K), dtype=np.int8)
+    lim = {8: 24, 6: 32, 4: 8}[bw]  # weights inside the bit width's range
+    bt_h = rng.integers(-lim, lim + (1 if bw == 8 else 0), size=(N, K), dtype=np.int8)
     bt = DeviceArray.from_host(bt_h)
     col_h = bt_h.astype(np.int64).sum(axis=1)
     col = DeviceArray.from_host(col_h)
@@ -37,7 +38,11 @@ def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, ker
     colterm = DeviceArray.from_host((col_h * zpa).astype(np.int32))
     for k in ("NQK_NO_PROJ", "NQK_NO_F32X", "NQK_NO_PG", "NQK_PG_NORESID"):
         monkeypatch.delenv(k, raising=False)
-    monkeypatch.setenv("NQK_NO_PROJ", "1")
+    monkeypatch.delenv("NQK_PROJ_RESID", raising=False)
+    if proj:  # the round-2 persistent 256 x 256 kernel (k_proj) for the residual epilogue
+        monkeypatch.setenv("NQK_PROJ_RESID", "1")
+    else:
+        monkeypatch.setenv("NQK_NO_PROJ", "1")
     monkeypatch.setenv("NQK_PG_WM", str(kernel))
     if no_f32x:
         monkeypatch.setenv("NQK_NO_F32X", "1")
@@ -56,7 +61,7 @@ def _run(epi_name, M, N, K, s_out_scale, use_pg, no_f32x, monkeypatch, seed, ker
         for g in range(3):
             e.s_acc[g] = float(np.float32(sa * (g + 1)))
             e.s_out[g] = (0.0021, 0.0173, 0.05)[g] * s_out_scale
-            e.zp_out[g], e.out[g] = (3, -140, 0)[g], bufs[g].ptr
+            e.zp_out[g], e.out[g] = (3, -140, 0)[g] if bw == 8 else (3, -20, 0)[g], bufs[g].ptr
     elif epi == EPI_RESID:
         e.group_cols = 1 << 30
         bufs = [DeviceArray((M, N), np.float32)]
@@ -178,5 +183,32 @@ def test_pg_resid_k3072_f32_dequant_from_column_l1_bound(M, seed, monkeypatch):
     k1, f32, _ = _run("resid", M, 768, 3072, 1.0, True, False, monkeypatch, seed, 1, l1=True)
     k2, f64, _ = _run("resid", M, 768, 3072, 1.0, True, True, monkeypatch, seed, 1, l1=True)
     assert (k1, k2) == (4, 4), (k1, k2)
+    for x, y in zip(f32, f64):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("epi_name,M,N,K,s_out_scale", [
+    ("qkv", 128 * 197, 2304, 768, 1.0), ("qkv", 300, 2304, 768, 0.05),
+    ("gelu", 128 * 50, 3072, 768, 1.0), ("gelu", 300, 3072, 768, 0.1),
+])
+def test_pg_gemm_bw6_equals_big_tile(epi_name, M, N, K, s_out_scale, monkeypatch):
+    """bit widths below 8 (here 6: int8 storage, the 6-bit output clamps of the QKV
+    blo/bhi and the GELU qlo/qhi) on k_pg equal k_qgemm_big bit for bit."""
+    seed = M + N + K + 6
+    k0, ref, _ = _run(epi_name, M, N, K, s_out_scale, False, False, monkeypatch, seed, 1, bw=6)
+    k1, got, _ = _run(epi_name, M, N, K, s_out_scale, True, False, monkeypatch, seed, 1, bw=6)
+    assert (k0, k1) == (1, 4), (k0, k1)
+    for x, y in zip(ref, got):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("M,seed", [(256 * 197, 21), (256 * 4, 22)])
+def test_proj_resid_k3072_f32_dequant_equals_f64(M, seed, monkeypatch):
+    """the round-2 persistent residual kernel (k_proj, NQK_PROJ_RESID=1) at K = 3072,
+    reachable in f32 through the column-L1 bound (col_l1max), equals its f64-dequantize run
+    (NQK_NO_F32X=1) bit for bit."""
+    k1, f32, _ = _run("resid", M, 768, 3072, 1.0, False, False, monkeypatch, seed, 1, l1=True, proj=True)
+    k2, f64, _ = _run("resid", M, 768, 3072, 1.0, False, True, monkeypatch, seed, 1, l1=True, proj=True)
+    assert (k1, k2) == (3, 3), (k1, k2)
     for x, y in zip(f32, f64):
         np.testing.assert_array_equal(x, y)

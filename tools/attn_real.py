@@ -54,6 +54,11 @@ print(f"image 0 head 0: scores span {sc.min():.3f} .. {sc.max():.3f}; min over r
       f"{(sc.min(1) - sc.max(1)).min():.3f}", flush=True)
 
 libs = {"main": _lib.load()}
+# AM_ENV="name:VAR=val,...;..." environment variants of the main build (read by the launcher per call)
+envs = {}
+for item in filter(None, os.environ.get("AM_ENV", "").split(";")):
+    name, kv = item.split(":", 1)
+    envs[name] = dict(x.split("=", 1) for x in kv.split(","))
 for item in filter(None, os.environ.get("AM_LIBS", "").split(",")):
     name, path = item.split("=", 1)
     lib = ctypes.CDLL(os.path.abspath(path))
@@ -83,11 +88,21 @@ def timed(lib):
     return 1e3 * ms.value / REPS
 
 
-res = {n: [] for n in libs}
+variants = [(n, lib, {}) for n, lib in libs.items()] + [(f"main:{n}", libs["main"], e) for n, e in envs.items()]
+res = {v[0]: [] for v in variants}
 ref = None
 for _ in range(ROUNDS):
-    for n, lib in libs.items():
-        res[n].append(timed(lib))
+    for n, lib, env in variants:
+        old = {kk: os.environ.get(kk) for kk in env}
+        os.environ.update(env)
+        try:
+            res[n].append(timed(lib))
+        finally:
+            for kk, vv in old.items():
+                if vv is None:
+                    os.environ.pop(kk, None)
+                else:
+                    os.environ[kk] = vv
         out = ctx.to_host()
         ref = out if ref is None else ref
         if not np.array_equal(out, ref):
@@ -95,7 +110,7 @@ for _ in range(ROUNDS):
 for n, ts in res.items():
     print(f"attention[{n}] (bench data, last layer, B={B}): min {min(ts):.1f} us  med {sorted(ts)[len(ts) // 2]:.1f} us",
           flush=True)
-    fn = getattr(libs[n], "nqk_attn_diag_stats", None)
+    fn = getattr(libs.get(n), "nqk_attn_diag_stats", None)
     if fn is not None:
         st = (ctypes.c_ulonglong * 4)()
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]

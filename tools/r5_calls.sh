@@ -43,4 +43,61 @@ r5_b() {
   echo done >> $STATUS
 }
 
+r5_c() {
+  # LayerNorm non-temporal row loads (whole-bench A/B, 3 interleaved reps); the
+  # attention's parked cycles (item 2): diagnostic builds without the workgroup barriers (1024), the
+  # Q loads (2048), the K / V loads (64), all three (3136), timed on the bench's data in one
+  # process, then PMC (wave cycles, parked, issue-stalled) per build, each under its own pass
+  rm -f $STATUS
+  AB_LIBS="main lnnt" AB_REPS=3 OUT=c timeout -k 10 900 bash tools/ab.sh
+  step ab_ln $?
+  AM_LIBS=a1024=tools/diag/libnqk_a1024.so,a2048=tools/diag/libnqk_a2048.so,a64=tools/diag/libnqk_a64.so,a3136=tools/diag/libnqk_a3136.so \
+    timeout -k 10 300 python -u tools/attn_real.py > gpurun_out/c_attn_real.txt 2>&1
+  step attn_real $?
+  LIB=numpy-quant_amd/numpy_quant/libnqk.so
+  cp $LIB /tmp/libnqk_main.so
+  for v in main a1024 a2048 a64; do
+    if [ $v = main ]; then cp /tmp/libnqk_main.so $LIB; else cp tools/diag/libnqk_$v.so $LIB; fi
+    rm -rf gpurun_out/c_pmc_$v
+    timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_INSTS_LDS \
+      --kernel-trace -d gpurun_out/c_pmc_$v -o run --output-format csv -- python -u tools/attn_real.py > gpurun_out/c_pmc_$v.log 2>&1
+    rc=$?
+    cp /tmp/libnqk_main.so $LIB
+    step pmc_$v $rc
+  done
+  echo done >> $STATUS
+}
+
+r5_d() {
+  # persistent attention with wave 3 prefetching the next (image, head) pair (NQK_ATTN_PF, default
+  # on): parity, then on the bench's data against the one-pair-per-workgroup form (NQK_ATTN_PF=0)
+  # and the V-only prefetch build (pfv), then PMC (parked / issue-stalled cycles) of each
+  rm -f $STATUS
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_b256.py tests/test_gpu_glut.py tests/test_gpu_fused_kernels.py \
+    tests/test_gpu_pgemm.py::test_pg_gemm_vit_tiny_shapes tests/test_gpu_plan.py -x -q --timeout 300 \
+    --timeout-method thread > gpurun_out/d_tests.log 2>&1
+  step tests $?
+  # K = 192 with the weight panel resident (NQK_PG_RB, default on) vs streamed, ViT-Ti whole bench
+  for rep in 1 2; do
+    for v in rb norb wn1; do
+      e=""; [ $v = norb ] && e="NQK_PG_RB=0"; [ $v = wn1 ] && e="NQK_EMBED_WN1=1"
+      env $e timeout -k 10 300 python -u bench.py --config vit_tiny --no-cpu-baseline --steps 20 > gpurun_out/d_tiny_${v}_$rep.json 2> gpurun_out/d_tiny_${v}_$rep.err
+      step tiny_$v $?
+    done
+  done
+  AM_LIBS=pfv=tools/diag/libnqk_pfv.so AM_ENV="nopf:NQK_ATTN_PF=0" timeout -k 10 300 python -u tools/attn_real.py \
+    > gpurun_out/d_attn_real.txt 2>&1
+  step attn_real $?
+  for v in pf nopf; do
+    e=""; [ $v = nopf ] && e="NQK_ATTN_PF=0"
+    rm -rf gpurun_out/d_pmc_$v
+    env $e timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_INSTS_LDS \
+      --kernel-trace -d gpurun_out/d_pmc_$v -o run --output-format csv -- python -u tools/attn_real.py > gpurun_out/d_pmc_$v.log 2>&1
+    step pmc_$v $?
+  done
+  AB_ENVS="nopf:NQK_ATTN_PF=0" AB_REPS=2 OUT=d timeout -k 10 600 bash tools/ab.sh
+  step ab $?
+  echo done >> $STATUS
+}
+
 "r5_$1"
