@@ -283,7 +283,7 @@ int nqk_pack_pg(const int8_t* bt, int8_t* out, int64_t N, int64_t K, int64_t ldb
  * x 32 bytes each, ceil(N/256)*256*K/2 bytes; k_pg unpacks them in registers after the LDS stage
  * (nqk_epilogue.b_packed = 2 with bt_pg = this image).  BASELINE configs[4]. */
 int nqk_pack_pg4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t ldb, int layout);
-/* The FFN-up epilogue's GELU chain as a table (round 4): model.py Div -> Erf -> Add -> Mul ->
+/* The FFN-up epilogue's GELU chain as a table (round 4; up to 1024 entries since round 5): model.py Div -> Erf -> Add -> Mul ->
  * Mul on f32 (numpy_helper.py:95-112 erf) followed by numpy_quantization.py:24-34 quantize
  * with (s_out, zp_out, bit_width), as a step function of the dequantized, biased f32 value h:
  * at most 1024 buckets of 8 bytes in lut (an 8 KiB, 16-byte aligned device buffer), the bucket

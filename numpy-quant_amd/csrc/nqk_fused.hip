@@ -1519,14 +1519,36 @@ k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float
 // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) combine and the leaf tree are xor-butterflies
 // (float addition is commutative, only the grouping matters).  2*NL lanes per row,
 // 64 / (2*NL) rows per wave; every load and store is 16 / 4 bytes per lane.
+// LayerNorm output quantize (numpy_quantization.py:24-34): t = RN32(RN64(y rs)) exactly as the
+// reference's f64 product, then q = rint(clip(zp + t, lo, hi)) by the magic number instead of
+// f64 arithmetic (round 5): c = med3(t, lo - zp, hi - zp) clamps in t's space (integer bounds:
+// the same as clamping zp + t), and RN32(c + 1.5 2^23 + zp) lies in [2^23, 2^24), where the f32
+// spacing is 1, so it is rint(c + zp) with ties to even (1.5 2^23 is even) — the low byte of its
+// bits is the output byte.  Exact for |zp| <= 2^20 and bit widths <= 8 (host-checked, LNQ);
+// 3 f32 + 2 f64-rate instructions per element instead of 9 mostly f64-rate ones.
+struct LnQ {
+  float qlo, qhi, magic;
+};
+__device__ __forceinline__ uint32_t ln_quant4(const float (&y)[4], double rs, const LnQ& m) {
+  float sv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float t = (float)((double)y[k] * rs);
+    sv[k] = __builtin_amdgcn_fmed3f(t, m.qlo, m.qhi) + m.magic;
+  }
+  const uint32_t x01 = __builtin_amdgcn_perm(__float_as_uint(sv[1]), __float_as_uint(sv[0]), 0x0c0c0400u);
+  const uint32_t x23 = __builtin_amdgcn_perm(__float_as_uint(sv[3]), __float_as_uint(sv[2]), 0x04000c0cu);
+  return x01 | x23;
+}
+
 #ifndef NQK_LN_LB
 #define NQK_LN_LB 1
 #endif
-template <int NL>
+template <int NL, bool MQ = false>
 __global__ void __launch_bounds__(256, NQK_LN_LB)
 k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
                int8_t* __restrict__ out, int64_t rows, float eps, float s, double rs, double zp, double lo,
-               double hi) {
+               double hi, LnQ mq) {
   constexpr int LF = 96, LPR = NL * 2, NI = LF / 8, COLS = NL * LF;
   const int lane = threadIdx.x & 63;
   const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
@@ -1578,12 +1600,16 @@ k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const f
     const float y[4] = {((xv[i].x * inv) * gg.x) + bb.x, ((xv[i].y * inv) * gg.y) + bb.y,
                         ((xv[i].z * inv) * gg.z) + bb.z, ((xv[i].w * inv) * gg.w) + bb.w};
     uint32_t packed = 0;
+    if constexpr (MQ) {
+      packed = ln_quant4(y, rs, mq);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float t = (float)((double)y[k] * rs);
-      const double uu = zp + (double)t;
-      const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
-      packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+      for (int k = 0; k < 4; ++k) {
+        const float t = (float)((double)y[k] * rs);
+        const double uu = zp + (double)t;
+        const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
+        packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+      }
     }
     *reinterpret_cast<uint32_t*>(orow + 8 * i) = packed;
   }
@@ -1603,11 +1629,11 @@ k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const f
 #ifndef NQK_LN_NT
 #define NQK_LN_NT 0  // 1: the f32 row loads non-temporal (read once; A/B variant, round 5)
 #endif
-template <int NL>
+template <int NL, bool MQ = false>
 __global__ void __launch_bounds__(256)
 k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
                int8_t* __restrict__ out, int64_t rows, float eps, float s, double rs, double zp, double lo,
-               double hi) {
+               double hi, LnQ mq) {
   constexpr int LF = 96, LPR = NL * 2, NI = LF / 8, COLS = NL * LF, RW = 64 / LPR;
   constexpr int CH = COLS / 4;                      // 16-B chunks per row
   constexpr int RSI = COLS * 4 + NL * 16;           // LDS bytes per input row
@@ -1683,12 +1709,16 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
     const float y[4] = {((xv[i].x * inv) * gg.x) + bb.x, ((xv[i].y * inv) * gg.y) + bb.y,
                         ((xv[i].z * inv) * gg.z) + bb.z, ((xv[i].w * inv) * gg.w) + bb.w};
     uint32_t packed = 0;
+    if constexpr (MQ) {
+      packed = ln_quant4(y, rs, mq);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float t = (float)((double)y[k] * rs);
-      const double uu = zp + (double)t;
-      const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
-      packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+      for (int k = 0; k < 4; ++k) {
+        const float t = (float)((double)y[k] * rs);
+        const double uu = zp + (double)t;
+        const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, lo), hi));
+        packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+      }
     }
     *reinterpret_cast<uint32_t*>(wl + r * RSO + c0 + 8 * i) = packed;
   }
@@ -2065,6 +2095,9 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
   const bool al = ((((uintptr_t)x) | ((uintptr_t)gamma) | ((uintptr_t)beta)) & 15) == 0 && (((uintptr_t)out) & 3) == 0;
   if (eq && snormal && al && (p.nleaf == 8 || p.nleaf == 4 || p.nleaf == 2)) {
     const double rs = 1.0 / (double)scale;
+    // the magic-number quantize (ln_quant4) where it is exact; NQK_LN_F64Q=1 keeps the f64 chain
+    const bool mq = bit_width >= 1 && bit_width <= 8 && zp >= -(1 << 20) && zp <= (1 << 20) && !getenv("NQK_LN_F64Q");
+    const LnQ lq{(float)(lo - (double)zp), (float)(hi - (double)zp), 0x1.8p23f + (float)zp};
     const int64_t lanes = rows * p.nleaf * 2;
     const unsigned grid = (unsigned)((lanes + 255) / 256);
     if (!getenv("NQK_LN_REG")) {  // rows through LDS: linear 1 KiB loads / stores per wave
@@ -2072,8 +2105,12 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
       const int64_t rpw = 128 / p.nleaf;
       const unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
 #define LNL(NLV)                                                                                                   \
-  hipLaunchKernelGGL((k_ln_quant_lds<NLV>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma, beta, out, \
-                     rows, eps, scale, rs, (double)zp, lo, hi)
+  if (mq)                                                                                                          \
+    hipLaunchKernelGGL((k_ln_quant_lds<NLV, true>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma,    \
+                       beta, out, rows, eps, scale, rs, (double)zp, lo, hi, lq);                                   \
+  else                                                                                                             \
+    hipLaunchKernelGGL((k_ln_quant_lds<NLV>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma, beta,    \
+                       out, rows, eps, scale, rs, (double)zp, lo, hi, lq)
       switch (p.nleaf) {
         case 8: LNL(8); break;
         case 4: LNL(4); break;
@@ -2084,11 +2121,11 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
     }
     switch (p.nleaf) {
       case 8: hipLaunchKernelGGL((k_ln_quant_reg<8>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
-                                 eps, scale, rs, (double)zp, lo, hi); break;
+                                 eps, scale, rs, (double)zp, lo, hi, lq); break;
       case 4: hipLaunchKernelGGL((k_ln_quant_reg<4>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out, rows,
-                                 eps, scale, rs, (double)zp, lo, hi); break;
+                                 eps, scale, rs, (double)zp, lo, hi, lq); break;
       default: hipLaunchKernelGGL((k_ln_quant_reg<2>), dim3(grid), dim3(256), 0, stream(), x, gamma, beta, out,
-                                  rows, eps, scale, rs, (double)zp, lo, hi); break;
+                                  rows, eps, scale, rs, (double)zp, lo, hi, lq); break;
     }
     return launch_status("nqk_ln_quant(reg)");
   }

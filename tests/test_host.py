@@ -300,3 +300,28 @@ def test_fused_away_value_raises_on_read():
         np.asarray(v)
     assert not isinstance(FusedAwayError("m"), AttributeError)
     assert getattr(v, "__array_interface__", None) is None
+
+
+@pytest.mark.parametrize("bw", [2, 4, 8])
+def test_ln_magic_quantize_equals_f64_chain(bw):
+    """The LayerNorm kernels' output quantize (nqk_fused.hip ln_quant4, round 5) restated in NumPy
+    f32 arithmetic: c = med3(t, lo - zp, hi - zp), s = RN32(c + 1.5 2^23 + zp), the low byte of
+    bits(s) — equal to the reference's rint(clip(zp + t, lo, hi)) in f64 (numpy_quantization.py:
+    24-34) for every t tried: exact half-integers (ties to even with odd and even zero points),
+    their neighbouring floats, the clamp bounds, infinities and random values, |zp| <= 2^20."""
+    lo, hi = -(2 ** (bw - 1)), 2 ** (bw - 1) - 1
+    rng = np.random.default_rng(bw)
+    for zp in (-(1 << 20), -300, -129, -128, -7, -1, 0, 1, 2, 3, 127, 140, 1 << 20):
+        k = np.arange(lo - zp - 3, hi - zp + 4, dtype=np.float64)
+        half = (k + 0.5).astype(np.float32)
+        t = np.concatenate([half, np.nextafter(half, np.float32(np.inf)), np.nextafter(half, np.float32(-np.inf)),
+                            k.astype(np.float32), (rng.standard_normal(20000) * (hi - lo)).astype(np.float32) - zp,
+                            np.array([np.inf, -np.inf, 3e38, -3e38], np.float32)]).astype(np.float32)
+        ref = np.rint(np.clip(np.float64(zp) + t.astype(np.float64), lo, hi)).astype(np.int64)
+        qlo, qhi = np.float32(lo - zp), np.float32(hi - zp)
+        magic = np.float32(1.5 * 2 ** 23) + np.float32(zp)
+        c = np.minimum(np.maximum(t, qlo), qhi)
+        s = (c + magic).astype(np.float32)
+        got = (s.view(np.uint32) & 0xFF).astype(np.int64)
+        got = np.where(got >= 128, got - 256, got)
+        np.testing.assert_array_equal(got, ref, err_msg=f"zp {zp}")
