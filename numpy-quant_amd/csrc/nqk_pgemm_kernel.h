@@ -63,10 +63,15 @@ constexpr int PG_TR_ROW = 272;  // bytes per staged residual row (256 + 16: conf
 // waves 4..7 rows 128..255 of the tile, both halves reading the SAME B stage: 32 KiB per k step
 // per CU for 2 x 128 x 256 outputs instead of 2 x 24 KiB (the operand stream measured ~1/3 of
 // FFN-down's time, profiles/r04_pg_operand_probe.txt); the residual transposes get their own LDS
+#ifndef NQK_PG_WM2_RD
+#define NQK_PG_WM2_RD 3  // ring depth of the 256 x 256 form's non-residual instances (4 fits its LDS)
+#endif
+// ring depth: 3 stages, or NQK_PG_WM2_RD for the 256 x 256 form where K is a multiple of 4 k steps
+constexpr int pg_rd(int epi, int wm, int nk) { return (wm == 2 && epi != PG_RESID && nk % 4 == 0) ? NQK_PG_WM2_RD : PG_RD; }
 constexpr int pg_stg(bool b4, int wm = 1) { return PG_ASTG * wm + PG_BN * (b4 ? PG_BK / 2 : PG_BK); }
-constexpr int pg_colp(bool b4, int wm = 1) { return PG_RD * pg_stg(b4, wm); }
-constexpr int pg_lds_bytes(int epi, bool b4, int wm = 1) {
-  return pg_colp(b4, wm) + 4096 + (epi == PG_GLUT ? 8 * (wm == 2 ? GLUT_MAX : GLUT_CAP1) : 0) +
+constexpr int pg_colp(bool b4, int wm = 1, int rd = PG_RD) { return rd * pg_stg(b4, wm); }
+constexpr int pg_lds_bytes(int epi, bool b4, int wm = 1, int nk = 12) {
+  return pg_colp(b4, wm, pg_rd(epi, wm, nk)) + 4096 + (epi == PG_GLUT ? 8 * (wm == 2 ? GLUT_MAX : GLUT_CAP1) : 0) +
          ((b4 || wm == 2) && epi == PG_RESID ? 4 * wm * 16 * PG_TR_ROW : 0);
 }
 
@@ -376,7 +381,9 @@ template <int EPI, int NK, bool F32X, bool B4, bool S8 = false, int WM = 1, bool
 __global__ void __launch_bounds__(256 * WM, 2 / WM)
 k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
      PgEpi e) {
-  static_assert(NK % PG_RD == 0 && (NK >= 2 * PG_RD || NK == PG_RD), "k_pg: NK a multiple of the ring depth");
+  constexpr int RD = RB ? PG_RD : pg_rd(EPI, WM, NK);  // ring stages
+  static_assert(NK % RD == 0 && (NK >= 2 * RD || NK == RD), "k_pg: NK a multiple of the ring depth");
+  static_assert(RD == PG_RD || EPI != PG_RESID, "k_pg: the residual epilogue borrows ring slot 2 (3 stages)");
   static_assert(WM == 1 || WM == 2, "k_pg: one or two 128-row halves per tile");
   static_assert(!RB || (NK == PG_RD && !B4 && EPI != PG_RESID), "k_pg<RB>: K = 3 k steps, int8, not residual");
   constexpr bool RESID = EPI == PG_RESID;
@@ -384,7 +391,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   constexpr int ASTG = PG_ASTG * WM;            // A bytes of a stage
   constexpr int BROW = B4 ? PG_BK / 2 : PG_BK;  // bytes of one B row per k-step
   constexpr int NBP = (B4 ? 2 : 4) / WM;        // B LDS-DMA pieces per wave per stage
-  constexpr int STG = pg_stg(B4, WM), COLP = pg_colp(B4, WM), LUTO = COLP + 4096;
+  constexpr int STG = pg_stg(B4, WM), COLP = pg_colp(B4, WM, RD), LUTO = COLP + 4096;
   constexpr int PW = 2 + NBP;                   // LDS-DMA pieces per wave per stage
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int lane = threadIdx.x & 63;
@@ -906,8 +913,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   // (WM = 2: the 8 KiB of a table of up to GLUT_MAX entries, 1 KiB per wave as well)
   if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
   issue_colp(cur.tn, 0);
-  issue_stage(cur, 0, 0);
-  issue_stage(cur, 1, 1);
+  sfor<0, RD - 1>([&](auto S) __attribute__((always_inline)) { issue_stage(cur, decltype(S)::value, decltype(S)::value); });
   if constexpr (NQK_PG_PRIO == 2) {
     if ((int)blockIdx.x >= G / 2) __builtin_amdgcn_s_setprio(1);
   }
@@ -917,10 +923,10 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     const bool more = it + 1 < iters;
     const Src nxt = src_of(tile_at(more ? it + 1 : it));
     const int cs = it & 1;
-    // stage 0 and this tile's column constants landed (younger: stage 1, the previous
+    // stage 0 and this tile's column constants landed (younger: stages 1 .. RD - 2, the previous
     // epilogue's operations)
-    if (it == 0) pg_vmcnt<PWA>();
-    else pg_vmcnt<PWA + EOPS>();
+    if (it == 0) pg_vmcnt<(RD - 2) * PWA>();
+    else pg_vmcnt<(RD - 2) * PWA + EOPS>();
     if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     // initial accumulators: minus the zero-point column terms of the lane's 16 columns
@@ -944,7 +950,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     for (int j = 0; j < 4; ++j) cinit[j] = B4 ? -(cinit[j] << 4) : -cinit[j];
     sfor<0, NK>([&](auto KT) __attribute__((always_inline)) {
       constexpr int kt = decltype(KT)::value;
-      constexpr int slot = kt % PG_RD;
+      constexpr int slot = kt % RD;
       v4i(&bc)[4] = B4 ? b0 : ((kt & 1) ? b1 : b0);
       v4i(&bn)[4] = (kt & 1) ? b0 : b1;
       v2u(&pc)[4] = (kt & 1) ? p1 : p0;
@@ -958,27 +964,29 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         }
       }
       // first half: subtiles 0..3; between the MFMAs the second half's A fragments and the
-      // refill of the slot step kt - 1 read (stage kt + 2)
+      // refill of the slot step kt - 1 read (stage kt + RD - 1)
       half(ic<0>{}, std::integral_constant<bool, kt == 0>{}, a_lo, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
         constexpr int q = decltype(Q)::value;
         if constexpr (q < 4) rd_a(a_hi, ic<slot>{}, ic<4>{}, Q);
         // stage kt + 2: NQK_PG_SPREAD 0 = all pieces after MFMA 4; 1 = one piece every
         // other MFMA from MFMA 1 (a burst of LDS-DMA issues costs each piece more:
         // MI355X_MICROARCH.md, LDS-DMA piece issue cost)
-        if constexpr (kt + 2 < NK) {
+        if constexpr (kt + RD - 1 < NK) {
           if constexpr (NQK_PG_SPREAD == 0) {
-            if constexpr (q == 4) issue_stage(cur, kt + 2, (kt + 2) % PG_RD);
+            if constexpr (q == 4) issue_stage(cur, kt + RD - 1, (kt + RD - 1) % RD);
           } else if constexpr ((q & 1) == 1 && (q >> 1) < PW) {
-            issue_piece(cur, kt + 2, (kt + 2) % PG_RD, q >> 1);
+            issue_piece(cur, kt + RD - 1, (kt + RD - 1) % RD, q >> 1);
           }
         }
       });
       if constexpr (kt == 1) issue_colp(nxt.tn, cs ^ 1);
       if constexpr (kt + 1 < NK) {
-        // stage kt + 1 landed; younger: stage kt + 2 (if issued), colp (step 1), and for
-        // stage 1 the previous tile's epilogue operations
-        constexpr int y = (kt + 2 < NK ? PWA : 0) + ((kt == 1 || kt == 2) ? 1 : 0);
-        if (kt == 0 && it > 0) pg_vmcnt<y + EOPS>();
+        // stage kt + 1 landed; younger: stages kt + 2 .. kt + RD - 1 (those issued), colp (step 1,
+        // after stage RD), and for the stages issued before this tile (kt + 1 <= RD - 2) the
+        // previous tile's epilogue operations
+        constexpr int hi_s = (kt + RD - 1 < NK ? kt + RD - 1 : NK - 1);
+        constexpr int y = (hi_s >= kt + 2 ? (hi_s - kt - 1) * PWA : 0) + ((kt >= 1 && kt <= RD - 1) ? 1 : 0);
+        if (kt + 1 <= RD - 2 && it > 0) pg_vmcnt<y + EOPS>();
         else pg_vmcnt<y>();
         pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
         if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
@@ -989,10 +997,10 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       half(ic<1>{}, std::integral_constant<bool, kt == 0>{}, a_hi, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
         constexpr int q = decltype(Q)::value;
         if constexpr (kt + 1 < NK) {
-          if constexpr (q < 4) rd_a(a_lo, ic<(kt + 1) % PG_RD>{}, ic<0>{}, Q);
+          if constexpr (q < 4) rd_a(a_lo, ic<(kt + 1) % RD>{}, ic<0>{}, Q);
           else if constexpr (q < 8) {
-            if constexpr (B4) rd_b4(pn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
-            else rd_b(bn, ic<(kt + 1) % PG_RD>{}, ic<q - 4>{});
+            if constexpr (B4) rd_b4(pn, ic<(kt + 1) % RD>{}, ic<q - 4>{});
+            else rd_b(bn, ic<(kt + 1) % RD>{}, ic<q - 4>{});
           }
         }
       });
@@ -1007,8 +1015,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     }
     // (the last tile re-stages its own first stages: never read, drained at the end; the
     // VMEM counts stay the same on every path)
-    issue_stage(nxt, 0, 0);
-    issue_stage(nxt, 1, 1);
+    sfor<0, RD - 1>([&](auto S) __attribute__((always_inline)) { issue_stage(nxt, decltype(S)::value, decltype(S)::value); });
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (NQK_PG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(1);
@@ -1050,7 +1057,7 @@ constexpr int pg_key(int epi, int nk, bool f32x, bool b4, bool s8, int wm, bool 
 }
 #define NQK_PG_CASE_RB(E, NKV, X, B, S, W, R)                                                                  \
   case pg_key(E, NKV, X, B, S, W, R):                                                                          \
-    hipLaunchKernelGGL((k_pg<E, NKV, X, B, S, W, R>), dim3(x.grid), dim3(256 * W), pg_lds_bytes(E, B, W), stream(), \
+    hipLaunchKernelGGL((k_pg<E, NKV, X, B, S, W, R>), dim3(x.grid), dim3(256 * W), pg_lds_bytes(E, B, W, NKV), stream(), \
                        x.a, x.bp, x.m, x.n, x.lda, x.tiles_n, x.ntiles, *static_cast<const PgEpi*>(x.epi));    \
     return true;
 #define NQK_PG_CASE(E, NKV, X, B, S, W) NQK_PG_CASE_RB(E, NKV, X, B, S, W, false)

@@ -132,14 +132,14 @@ for name in sel:
     variants = []
     for lname, lib in libs.items():
         variants.append((f"pg:{lname}", lib, {}, True))
-    for vname, env in envs.items():
-        variants.append((f"pg:{vname}", main, env, True))
+    for vname, env in envs.items():  # (PGM_ENV variants: of every build)
+        for lname, lib in libs.items():
+            variants.append((f"pg:{vname}" if lname == "main" else f"pg:{lname}:{vname}", lib, env, True))
     if keep[-1] is not None:
         for lname, lib in libs.items():
             variants.append(("glut" if lname == "main" else f"glut:{lname}", lib, {}, "glut"))
-    variants.append(("pg:wm2", main, {"NQK_PG_WM": "2"}, True))
-    if keep[-1] is not None:
-        variants.append(("glut:wm2", main, {"NQK_PG_WM": "2"}, "glut"))
+            for vname, env in envs.items():
+                variants.append((f"glut:{vname}" if lname == "main" else f"glut:{lname}:{vname}", lib, env, "glut"))
     variants.append(("r02", main, {"NQK_PROJ_GELU": "1"} if epi == 4 else {}, False))
     res = {v[0]: [] for v in variants}
     for _ in range(ROUNDS):

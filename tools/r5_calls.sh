@@ -100,4 +100,23 @@ r5_d() {
   echo done >> $STATUS
 }
 
+r5_f() {
+  # the 256 x 256 form with a 4-deep ring (tools/diag/libnqk_rd4.so, NQK_PG_WM2_RD=4) against the
+  # 3-deep one and the 128 x 256 form: parity of the 4-deep build (copied over the main library for
+  # its tests), then the per-shape micro (both builds, NQK_PG_WM=1 / 2)
+  rm -f $STATUS
+  LIB=numpy-quant_amd/numpy_quant/libnqk.so
+  cp $LIB /tmp/libnqk_main.so
+  cp tools/diag/libnqk_rd4.so $LIB
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_pgemm.py tests/test_gpu_glut.py -x -q --timeout 300 \
+    --timeout-method thread > gpurun_out/f_tests.log 2>&1
+  rc=$?
+  cp /tmp/libnqk_main.so $LIB
+  step tests_rd4 $rc
+  PGM_LIBS=rd4=tools/diag/libnqk_rd4.so PGM_ENV="wm2:NQK_PG_WM=2" PGM_SHAPES=qkv,up PGM_ROUNDS=3 \
+    timeout -k 10 400 python -u tools/pg_micro.py > gpurun_out/f_pg_micro.txt 2>&1
+  step pg_micro $?
+  echo done >> $STATUS
+}
+
 "r5_$1"
