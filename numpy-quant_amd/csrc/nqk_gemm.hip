@@ -233,6 +233,7 @@ struct EmbedEpi {
   const float* bias;
   const float* pos;  // [HW + 1][N]
   int64_t hw;
+  int xcd;  // k_embed_q: 1 = XCD-aware tile order (a row panel's column tiles on one XCD)
 };
 
 template <bool EMBED, bool AL16, bool VEC = false>
@@ -425,7 +426,19 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
   __shared__ __attribute__((aligned(16))) float sb[2][BN * EQ_ROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, r32 = lane & 31, h = lane >> 5;
-  const int64_t m0 = (int64_t)blockIdx.y * 128, n0 = (int64_t)blockIdx.x * BN;
+  // XCD-aware tile order (ee.xcd): blocks are dealt round-robin over the 8 XCDs (block b on XCD
+  // b % 8, MI355X_MICROARCH.md), so the row-panel-major tile ids are split into 8 contiguous bands,
+  // band x served by the blocks of XCD x: the column tiles of one row panel — which read the same
+  // image rows — share an L2 instead of fetching the image once per XCD
+  int64_t tm = blockIdx.y, tn = blockIdx.x;
+  if (ee.xcd) {
+    const int64_t gx = gridDim.x, T = gx * gridDim.y, b = (int64_t)blockIdx.y * gx + blockIdx.x;
+    const int64_t x = b % 8, q8 = T / 8, r8 = T % 8;
+    const int64_t tile = x * q8 + (x < r8 ? x : r8) + b / 8;
+    tm = tile / gx;
+    tn = tile - tm * gx;
+  }
+  const int64_t m0 = tm * 128, n0 = tn * BN;
   // A rows of this thread: patch m = image * hw + oy * wo + ox
   const int ar = tid & 127, hf = tid >> 7;
   const int64_t am = m0 + ar < M ? m0 + ar : M - 1;
@@ -897,13 +910,13 @@ extern "C" int nqk_sgemm_embed(const float* cols, const float* w, const float* b
   const bool vec = (N % 4) == 0 && ((((uintptr_t)cols) | ((uintptr_t)w)) & 15) == 0 && !getenv("NQK_SGEMM_SCALAR");
   if (kblocks_al16(K, kb) && vec)
     hipLaunchKernelGGL((k_sgemm_mfma<true, true, true>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1,
-                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
+                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
   else if (kblocks_al16(K, kb))
     hipLaunchKernelGGL((k_sgemm_mfma<true, true>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1, N,
-                       (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
+                       (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
   else
     hipLaunchKernelGGL((k_sgemm_mfma<true, false>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1,
-                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw});
+                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
   if (int rc = launch_status("nqk_sgemm_embed")) return rc;
   hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);
   return launch_status("nqk_sgemm_embed(cls)");
@@ -930,10 +943,10 @@ extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float
   // profiles/r04_embed_1wg_streams_dropped.txt)
   if (N % 128 == 0) {
     hipLaunchKernelGGL(k_embed_q<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
-                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw});
+                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
   } else {
     hipLaunchKernelGGL(k_embed_q<1>, dim3((unsigned)(N / 64), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
-                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw});
+                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
   }
   if (int rc = launch_status("nqk_embed_q")) return rc;
   hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);

@@ -119,4 +119,23 @@ r5_f() {
   echo done >> $STATUS
 }
 
+r5_g() {
+  # patch embedding with the XCD-aware tile order (default) vs the plain grid order
+  # (NQK_EMBED_NOXCD=1): the embedding parity tests, whole-bench A/B, then FETCH_SIZE of each
+  rm -f $STATUS
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_fused_kernels.py -k embed -x -q --timeout 200 \
+    --timeout-method thread > gpurun_out/g_tests.log 2>&1
+  step tests $?
+  AB_ENVS="noxcd:NQK_EMBED_NOXCD=1" AB_REPS=3 OUT=g timeout -k 10 900 bash tools/ab.sh
+  step ab $?
+  for v in xcd noxcd; do
+    e=""; [ $v = noxcd ] && e="NQK_EMBED_NOXCD=1"
+    rm -rf gpurun_out/g_pmc_$v
+    env $e NQK_SPLIT=0 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/g_pmc_$v -o run --output-format csv \
+      -- python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary > gpurun_out/g_pmc_$v.log 2>&1
+    step pmc_$v $?
+  done
+  echo done >> $STATUS
+}
+
 "r5_$1"
