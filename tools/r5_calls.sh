@@ -138,4 +138,20 @@ r5_g() {
   echo done >> $STATUS
 }
 
+r5_h() {
+  # stream parts of the fused forward (NQK_STREAMS = 2 default, 3, 4) for ViT-Ti and ViT-Base,
+  # whole bench, 2 interleaved reps each
+  rm -f $STATUS
+  for rep in 1 2; do
+    for cfg in vit_tiny vit; do
+      for n in 2 3 4; do
+        NQK_STREAMS=$n timeout -k 10 300 python -u bench.py --config $cfg --no-cpu-baseline --no-secondary --steps 20 \
+          > gpurun_out/h_${cfg}_s${n}_$rep.json 2> gpurun_out/h_${cfg}_s${n}_$rep.err
+        step ${cfg}_s$n $?
+      done
+    done
+  done
+  echo done >> $STATUS
+}
+
 "r5_$1"
