@@ -1529,12 +1529,17 @@ k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float
 struct LnQ {
   float qlo, qhi, magic;
 };
+template <bool PK = false>
 __device__ __forceinline__ uint32_t ln_quant4(const float (&y)[4], double rs, const LnQ& m) {
   float sv[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float t = (float)((double)y[k] * rs);
-    sv[k] = __builtin_amdgcn_fmed3f(t, m.qlo, m.qhi) + m.magic;
+  for (int k = 0; k < 4; ++k) sv[k] = __builtin_amdgcn_fmed3f((float)((double)y[k] * rs), m.qlo, m.qhi);
+  if constexpr (PK) {  // the magic-number adds as two packed pairs
+    const v2f_t s01 = v2f_t{sv[0], sv[1]} + v2f_t{m.magic, m.magic}, s23 = v2f_t{sv[2], sv[3]} + v2f_t{m.magic, m.magic};
+    sv[0] = s01[0], sv[1] = s01[1], sv[2] = s23[0], sv[3] = s23[1];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sv[k] = sv[k] + m.magic;
   }
   const uint32_t x01 = __builtin_amdgcn_perm(__float_as_uint(sv[1]), __float_as_uint(sv[0]), 0x0c0c0400u);
   const uint32_t x23 = __builtin_amdgcn_perm(__float_as_uint(sv[3]), __float_as_uint(sv[2]), 0x04000c0cu);
@@ -1626,17 +1631,33 @@ k_ln_quant_reg(const float* __restrict__ x, const float* __restrict__ g, const f
 // quantize chain, 40.9 vs 39.3 us per launch at 50432 x 768, profiles/r04_ln_filter_dropped.txt;
 // two row groups per wave with the second group's loads under the first's work, 40.8 vs
 // 39.7 us, profiles/r04_ln_gpw_dropped.txt.)
+#ifndef NQK_LN_PK
+#define NQK_LN_PK 1  // 1: the f32 element arithmetic of the LDS variant as packed pairs (round 5)
+#endif
 #ifndef NQK_LN_NT
 #define NQK_LN_NT 0  // 1: the f32 row loads non-temporal (read once; A/B variant, round 5)
 #endif
-template <int NL, bool MQ = false>
-__global__ void __launch_bounds__(256)
+#ifndef NQK_LN_DMA
+#define NQK_LN_DMA 1  // 1: the rows by LDS-DMA (buffer_load ... lds) into an XOR-swizzled image (round 5)
+#endif
+// NQK_LN_DMA: LDS-DMA writes a wave's 64 x 16 B contiguously, so the image cannot carry the
+// per-leaf pad; instead 16-B chunk c of row r sits at position c ^ 2 h (bits 1-2 flipped, inside
+// the leaf's aligned 8-chunk blocks: an involution), h = (leaf >> 1) & 3 for 8 leaves, r & 3 for
+// 4 and 2.  A tree read (chunk 24 leaf + 2 i + grp of each lane's row) then puts the 16 lanes of
+// every ds_read_b128 lane group on 16 different 4-bank slots (rows of 24 NL chunks = 0 mod 16;
+// checked for every i and lane group of MI355X_MICROARCH.md's table by tests/test_host.py)
+__host__ __device__ constexpr int ln_swz(int nl, int r, int c) {
+  return c ^ ((nl == 8 ? ((c / 24) >> 1) & 3 : r & 3) << 1);
+}
+template <int NL, bool MQ = false, int WPB = 4>  // WPB: waves (row groups) per workgroup
+__global__ void __launch_bounds__(64 * WPB)
 k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
                int8_t* __restrict__ out, int64_t rows, float eps, float s, double rs, double zp, double lo,
                double hi, LnQ mq) {
   constexpr int LF = 96, LPR = NL * 2, NI = LF / 8, COLS = NL * LF, RW = 64 / LPR;
   constexpr int CH = COLS / 4;                      // 16-B chunks per row
-  constexpr int RSI = COLS * 4 + NL * 16;           // LDS bytes per input row
+  constexpr bool DMA = NQK_LN_DMA;
+  constexpr int RSI = COLS * 4 + (DMA ? 0 : NL * 16);  // LDS bytes per input row
   constexpr int RSO = COLS + 16;                    // LDS bytes per output row
   constexpr int WLDS = RW * RSI;                    // >= RW * RSO
   constexpr int NLD = RW * CH / 64, NST = RW * COLS / 16 / 64;
@@ -1644,12 +1665,23 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int8_t* const wl = lds + wave * WLDS;
-  const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * RW;
+  const int64_t row0 = ((int64_t)blockIdx.x * WPB + wave) * RW;
   if (row0 >= rows) return;  // (uniform per wave; no workgroup barrier follows)
   // ---- linear loads (rows past the end read the last row; not stored)
+  if constexpr (DMA) {
+    // position P = 64 k + lane of the image <- row P / CH, chunk ln_swz(P % CH)
+    const rsrc_t rx = make_rsrc(x, (uint32_t)((uint64_t)rows * COLS * 4));
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int P = k * 64 + lane, r = P / CH, c = ln_swz(NL, r, P - r * CH);
+      const int64_t gr = row0 + r < rows ? row0 + r : rows - 1;
+      buf_lds16(rx, wl + k * 1024, (uint32_t)(gr * COLS + c * 4) * 4u, 0u);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   float4 ld[NLD];
 #pragma unroll
-  for (int k = 0; k < NLD; ++k) {
+  for (int k = 0; k < NLD && !DMA; ++k) {
     const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
     const int64_t gr = row0 + r < rows ? row0 + r : rows - 1;
     if constexpr (NQK_LN_NT) {
@@ -1661,11 +1693,11 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
     }
   }
 #pragma unroll
-  for (int k = 0; k < NLD; ++k) {
+  for (int k = 0; k < NLD && !DMA; ++k) {
     const int C = k * 64 + lane, r = C / CH, c = C - r * CH;
     *reinterpret_cast<float4*>(wl + r * RSI + c * 16 + (c / (LF / 4)) * 16) = ld[k];
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (!DMA) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
   // ---- the tree layout: lane (row r, leaf, grp) holds columns leaf*96 + 8i + 4grp + 0..3
   const int r = lane / LPR, u = lane % LPR, leaf = u >> 1, grp = u & 1;
@@ -1673,32 +1705,72 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
   float4 xv[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
-    xv[i] = *reinterpret_cast<const float4*>(wl + r * RSI + (leaf * (LF / 4) + 2 * i + grp) * 16 + leaf * 16);
-  float a0 = xv[0].x, a1 = xv[0].y, a2 = xv[0].z, a3 = xv[0].w;
+    xv[i] = *reinterpret_cast<const float4*>(
+        wl + r * RSI + (DMA ? ln_swz(NL, r, leaf * (LF / 4) + 2 * i + grp) * 16 : (leaf * (LF / 4) + 2 * i + grp) * 16 + leaf * 16));
+  float inv, nmean;
+  v2f_t xl[NI], xh[NI];  // NQK_LN_PK: xv[i] as the pairs (x, y), (z, w), centred in place
+  if constexpr (NQK_LN_PK) {
+    // element pairs as packed f32 (v_pk_add / v_pk_mul: per lane the same IEEE operations in
+    // the same order as the scalar form below, one issue slot for two elements)
 #pragma unroll
-  for (int i = 1; i < NI; ++i) {
-    a0 = a0 + xv[i].x; a1 = a1 + xv[i].y; a2 = a2 + xv[i].z; a3 = a3 + xv[i].w;
+    for (int i = 0; i < NI; ++i) {
+      xl[i] = v2f_t{xv[i].x, xv[i].y};
+      xh[i] = v2f_t{xv[i].z, xv[i].w};
+    }
+    v2f_t al = xl[0], ah = xh[0];
+#pragma unroll
+    for (int i = 1; i < NI; ++i) {
+      al = al + xl[i];
+      ah = ah + xh[i];
+    }
+    float acc = (al[0] + al[1]) + (ah[0] + ah[1]);
+#pragma unroll
+    for (int m = 1; m < LPR; m <<= 1) acc = acc + __shfl_xor(acc, m, 64);
+    nmean = -(acc / (float)COLS);
+    const v2f_t nm2 = v2f_t{nmean, nmean};
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      xl[i] = xl[i] + nm2;
+      xh[i] = xh[i] + nm2;
+    }
+    al = xl[0] * xl[0];
+    ah = xh[0] * xh[0];
+#pragma unroll
+    for (int i = 1; i < NI; ++i) {
+      al = al + xl[i] * xl[i];
+      ah = ah + xh[i] * xh[i];
+    }
+    float v2 = (al[0] + al[1]) + (ah[0] + ah[1]);
+#pragma unroll
+    for (int m = 1; m < LPR; m <<= 1) v2 = v2 + __shfl_xor(v2, m, 64);
+    inv = 1.0f / __builtin_sqrtf(v2 / (float)COLS + eps);
+  } else {
+    float a0 = xv[0].x, a1 = xv[0].y, a2 = xv[0].z, a3 = xv[0].w;
+  #pragma unroll
+    for (int i = 1; i < NI; ++i) {
+      a0 = a0 + xv[i].x; a1 = a1 + xv[i].y; a2 = a2 + xv[i].z; a3 = a3 + xv[i].w;
+    }
+    float acc = (a0 + a1) + (a2 + a3);
+  #pragma unroll
+    for (int m = 1; m < LPR; m <<= 1) acc = acc + __shfl_xor(acc, m, 64);
+    const float fcols = (float)COLS;
+    nmean = -(acc / fcols);
+  #pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      xv[i].x = xv[i].x + nmean; xv[i].y = xv[i].y + nmean; xv[i].z = xv[i].z + nmean; xv[i].w = xv[i].w + nmean;
+    }
+    a0 = xv[0].x * xv[0].x; a1 = xv[0].y * xv[0].y; a2 = xv[0].z * xv[0].z; a3 = xv[0].w * xv[0].w;
+  #pragma unroll
+    for (int i = 1; i < NI; ++i) {
+      a0 = a0 + xv[i].x * xv[i].x; a1 = a1 + xv[i].y * xv[i].y;
+      a2 = a2 + xv[i].z * xv[i].z; a3 = a3 + xv[i].w * xv[i].w;
+    }
+    float v2 = (a0 + a1) + (a2 + a3);
+  #pragma unroll
+    for (int m = 1; m < LPR; m <<= 1) v2 = v2 + __shfl_xor(v2, m, 64);
+    const float var = v2 / fcols;
+    inv = 1.0f / __builtin_sqrtf(var + eps);
   }
-  float acc = (a0 + a1) + (a2 + a3);
-#pragma unroll
-  for (int m = 1; m < LPR; m <<= 1) acc = acc + __shfl_xor(acc, m, 64);
-  const float fcols = (float)COLS;
-  const float nmean = -(acc / fcols);
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    xv[i].x = xv[i].x + nmean; xv[i].y = xv[i].y + nmean; xv[i].z = xv[i].z + nmean; xv[i].w = xv[i].w + nmean;
-  }
-  a0 = xv[0].x * xv[0].x; a1 = xv[0].y * xv[0].y; a2 = xv[0].z * xv[0].z; a3 = xv[0].w * xv[0].w;
-#pragma unroll
-  for (int i = 1; i < NI; ++i) {
-    a0 = a0 + xv[i].x * xv[i].x; a1 = a1 + xv[i].y * xv[i].y;
-    a2 = a2 + xv[i].z * xv[i].z; a3 = a3 + xv[i].w * xv[i].w;
-  }
-  float v2 = (a0 + a1) + (a2 + a3);
-#pragma unroll
-  for (int m = 1; m < LPR; m <<= 1) v2 = v2 + __shfl_xor(v2, m, 64);
-  const float var = v2 / fcols;
-  const float inv = 1.0f / __builtin_sqrtf(var + eps);
   // every lane's tree reads are done before the image is overwritten (in-order LDS)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
@@ -1706,11 +1778,19 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
   for (int i = 0; i < NI; ++i) {
     const float4 gg = *reinterpret_cast<const float4*>(g + c0 + 8 * i);
     const float4 bb = *reinterpret_cast<const float4*>(b + c0 + 8 * i);
-    const float y[4] = {((xv[i].x * inv) * gg.x) + bb.x, ((xv[i].y * inv) * gg.y) + bb.y,
-                        ((xv[i].z * inv) * gg.z) + bb.z, ((xv[i].w * inv) * gg.w) + bb.w};
+    float y[4];
+    if constexpr (NQK_LN_PK) {
+      const v2f_t i2 = v2f_t{inv, inv};
+      const v2f_t yl = ((xl[i] * i2) * v2f_t{gg.x, gg.y}) + v2f_t{bb.x, bb.y};
+      const v2f_t yh = ((xh[i] * i2) * v2f_t{gg.z, gg.w}) + v2f_t{bb.z, bb.w};
+      y[0] = yl[0], y[1] = yl[1], y[2] = yh[0], y[3] = yh[1];
+    } else {
+      y[0] = ((xv[i].x * inv) * gg.x) + bb.x, y[1] = ((xv[i].y * inv) * gg.y) + bb.y;
+      y[2] = ((xv[i].z * inv) * gg.z) + bb.z, y[3] = ((xv[i].w * inv) * gg.w) + bb.w;
+    }
     uint32_t packed = 0;
     if constexpr (MQ) {
-      packed = ln_quant4(y, rs, mq);
+      packed = ln_quant4<NQK_LN_PK>(y, rs, mq);
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -1732,7 +1812,134 @@ k_ln_quant_lds(const float* __restrict__ x, const float* __restrict__ g, const f
     if (row0 + rr < rows) *reinterpret_cast<v4i*>(out + (row0 + rr) * COLS + c * 16) = v;
   }
 }
-constexpr int ln_lds_bytes(int nl) { return 4 * (64 / (2 * nl)) * (nl * 96 * 4 + nl * 16); }
+// Persistent form (round 5, NQK_LN_PERS): one-wave workgroups, LN_PERS_W per CU, each walking
+// row groups g, g + grid, ... with the next group's rows loaded by LDS-DMA into the second half
+// of a double-buffered image while the current group is reduced, quantized and stored (the
+// single-shot kernel's waves load, then compute, then store: in a grid that is one or a few
+// waves per slot those phases line up across the chip).  gamma / beta stay in registers (a
+// lane's columns are the same in every group).  Same arithmetic as k_ln_quant_lds with
+// NQK_LN_PK / NQK_LN_DMA.
+template <int NL, bool MQ>
+__global__ void __launch_bounds__(64)
+k_ln_quant_pers(const float* __restrict__ x, const float* __restrict__ g, const float* __restrict__ b,
+                int8_t* __restrict__ out, int64_t rows, float eps, double rs, double zp, double lo, double hi, LnQ mq) {
+  constexpr int LF = 96, LPR = NL * 2, NI = LF / 8, COLS = NL * LF, RW = 64 / LPR;
+  constexpr int CH = COLS / 4, RSI = COLS * 4, RSO = COLS + 16, WLDS = RW * RSI;
+  constexpr int NLD = RW * CH / 64, NST = RW * COLS / 16 / 64;
+  static_assert(RW * CH % 64 == 0 && RW * COLS % 1024 == 0 && RW * RSO <= WLDS, "k_ln_quant_pers: shape");
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  const int lane = threadIdx.x;
+  const int64_t ngroups = (rows + RW - 1) / RW;
+  int64_t grp = blockIdx.x;
+  if (grp >= ngroups) return;
+  // rx0: an empty buffer (loads return 0, no memory access) for the pieces issued after the
+  // last group, so every iteration issues the same NLD pieces (uniform counted waits: the
+  // compiler's own wait for the previous stores' data registers is then vmcnt(NLD), not 0)
+  const rsrc_t rx = make_rsrc(x, (uint32_t)((uint64_t)rows * COLS * 4)), rx0 = make_rsrc(x, 0u);
+  auto issue = [&](int64_t gi, int8_t* img, rsrc_t rr) {
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      const int P = k * 64 + lane, r = P / CH, c = ln_swz(NL, r, P - r * CH);
+      const int64_t gr = gi * RW + r < rows ? gi * RW + r : rows - 1;
+      buf_lds16(rr, img + k * 1024, (uint32_t)(gr * COLS + c * 4) * 4u, 0u);
+    }
+  };
+  const int r = lane / LPR, u = lane % LPR, leaf = u >> 1, gq = u & 1;
+  const int c0 = leaf * LF + 4 * gq;
+  v2f_t gl[NI], gh[NI], bl[NI], bh[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const float4 gg = *reinterpret_cast<const float4*>(g + c0 + 8 * i);
+    const float4 bb = *reinterpret_cast<const float4*>(b + c0 + 8 * i);
+    gl[i] = v2f_t{gg.x, gg.y}, gh[i] = v2f_t{gg.z, gg.w}, bl[i] = v2f_t{bb.x, bb.y}, bh[i] = v2f_t{bb.z, bb.w};
+  }
+  // the parameters are in registers before any LDS-DMA is counted (the loop's waits are exact)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NI; ++i) asm volatile("" : "+v"(gl[i]), "+v"(gh[i]), "+v"(bl[i]), "+v"(bh[i]));
+  issue(grp, lds, rx);
+  for (int cur = 0; grp < ngroups; grp += gridDim.x, cur ^= 1) {
+    int8_t* const wl = lds + cur * WLDS;
+    const int64_t nxt = grp + gridDim.x;
+    // the other half held the previous group's staged output, read (lgkmcnt 0) before its stores;
+    // vmcnt(NLD): this group's pieces (and the previous group's stores, issued before the next
+    // pieces) are done, the next group's NLD pieces stay in flight
+    issue(nxt < ngroups ? nxt : grp, lds + (cur ^ 1) * WLDS, nxt < ngroups ? rx : rx0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD) : "memory");
+    __builtin_amdgcn_wave_barrier();
+    // the tree reads by inline asm, their lgkmcnt wait tied to the values: a compiler-visible LDS
+    // read is given an s_waitcnt vmcnt(0) for the LDS-DMA in flight (it cannot tell the halves
+    // apart), which would drain the next group's pieces
+    typedef float v4f_t __attribute__((ext_vector_type(4)));
+    v4f_t tv[NI];
+    static_assert(NI == 12, "k_ln_quant_pers: 12 tree reads");
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t a = (uint32_t)(uintptr_t)(lds_ptr_t)(wl + r * RSI + ln_swz(NL, r, leaf * (LF / 4) + 2 * i + gq) * 16);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(tv[i]) : "v"(a));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]), "+v"(tv[3]), "+v"(tv[4]), "+v"(tv[5]), "+v"(tv[6]),
+                   "+v"(tv[7]), "+v"(tv[8]), "+v"(tv[9]), "+v"(tv[10]), "+v"(tv[11])::"memory");
+    v2f_t xl[NI], xh[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) xl[i] = v2f_t{tv[i][0], tv[i][1]}, xh[i] = v2f_t{tv[i][2], tv[i][3]};
+    v2f_t al = xl[0], ah = xh[0];
+#pragma unroll
+    for (int i = 1; i < NI; ++i) al = al + xl[i], ah = ah + xh[i];
+    float acc = (al[0] + al[1]) + (ah[0] + ah[1]);
+#pragma unroll
+    for (int m = 1; m < LPR; m <<= 1) acc = acc + __shfl_xor(acc, m, 64);
+    const float nmean = -(acc / (float)COLS);
+    const v2f_t nm2 = v2f_t{nmean, nmean};
+#pragma unroll
+    for (int i = 0; i < NI; ++i) xl[i] = xl[i] + nm2, xh[i] = xh[i] + nm2;
+    al = xl[0] * xl[0], ah = xh[0] * xh[0];
+#pragma unroll
+    for (int i = 1; i < NI; ++i) al = al + xl[i] * xl[i], ah = ah + xh[i] * xh[i];
+    float v2 = (al[0] + al[1]) + (ah[0] + ah[1]);
+#pragma unroll
+    for (int m = 1; m < LPR; m <<= 1) v2 = v2 + __shfl_xor(v2, m, 64);
+    const float inv = 1.0f / __builtin_sqrtf(v2 / (float)COLS + eps);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tree reads done before the staging overwrites
+    __builtin_amdgcn_wave_barrier();
+    const v2f_t i2 = v2f_t{inv, inv};
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const v2f_t yl = ((xl[i] * i2) * gl[i]) + bl[i], yh = ((xh[i] * i2) * gh[i]) + bh[i];
+      const float y[4] = {yl[0], yl[1], yh[0], yh[1]};
+      uint32_t packed = 0;
+      if constexpr (MQ) {
+        packed = ln_quant4<true>(y, rs, mq);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float t = (float)((double)y[k] * rs);
+          const int q = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(zp + (double)t, lo), hi));
+          packed |= ((uint32_t)(q & 0xff)) << (8 * k);
+        }
+      }
+      *reinterpret_cast<uint32_t*>(wl + r * RSO + c0 + 8 * i) = packed;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int64_t row0 = grp * RW;
+    v4i sv[NST];
+#pragma unroll
+    for (int k = 0; k < NST; ++k) {
+      const int C = k * 64 + lane, rr = C / (COLS / 16), c = C - rr * (COLS / 16);
+      sv[k] = *reinterpret_cast<const v4i*>(wl + rr * RSO + c * 16);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before the next issue refills it
+#pragma unroll
+    for (int k = 0; k < NST; ++k) {
+      const int C = k * 64 + lane, rr = C / (COLS / 16), c = C - rr * (COLS / 16);
+      if (row0 + rr < rows) *reinterpret_cast<v4i*>(out + (row0 + rr) * COLS + c * 16) = sv[k];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the wave's LDS is released
+}
+constexpr int ln_lds_bytes(int nl, int wpb = 4) { return wpb * (64 / (2 * nl)) * (nl * 96 * 4 + (NQK_LN_DMA ? 0 : nl * 16)); }
 
 // ------------------------------------------------------------------ Softmax + quantize
 // one row per wave; output row stride ldo (>= cols, pad zero-filled); optional row sums
@@ -2100,22 +2307,49 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
     const LnQ lq{(float)(lo - (double)zp), (float)(hi - (double)zp), 0x1.8p23f + (float)zp};
     const int64_t lanes = rows * p.nleaf * 2;
     const unsigned grid = (unsigned)((lanes + 255) / 256);
-    if (!getenv("NQK_LN_REG")) {  // rows through LDS: linear 1 KiB loads / stores per wave
-      // 128 / nleaf rows per workgroup (4 waves of 64 / (2 nleaf) rows)
-      const int64_t rpw = 128 / p.nleaf;
+    // rows through LDS: linear 1 KiB loads / stores per wave (the LDS-DMA form addresses x by 32-bit
+    // buffer offsets: larger inputs take the register-tree kernel)
+    const bool dma_ok = !NQK_LN_DMA || rows * cols * 4 < (int64_t(1) << 31);
+    const char* pe = getenv("NQK_LN_PERS");
+    if (NQK_LN_DMA && dma_ok && pe && atoi(pe) > 0 && mq && !getenv("NQK_LN_REG")) {
+      // persistent double-buffered form: NQK_LN_PERS waves per CU (1-wave workgroups, 24 KiB each)
+      const int64_t ngroups = (rows + 32 / p.nleaf - 1) / (32 / p.nleaf);
+      const int64_t w = std::min<int64_t>(ngroups, (int64_t)std::min(6, atoi(pe)) * num_cus());
+      const int lb = 2 * (32 / p.nleaf) * p.nleaf * 96 * 4;
+#define LNP(NLV)                                                                                                 \
+  hipLaunchKernelGGL((k_ln_quant_pers<NLV, true>), dim3((unsigned)w), dim3(64), lb, stream(), x, gamma, beta, out, \
+                     rows, eps, rs, (double)zp, lo, hi, lq)
+      switch (p.nleaf) {
+        case 8: LNP(8); break;
+        case 4: LNP(4); break;
+        default: LNP(2); break;
+      }
+#undef LNP
+      return launch_status("nqk_ln_quant(pers)");
+    }
+    if (!getenv("NQK_LN_REG") && dma_ok) {
+      // WPB waves of 64 / (2 nleaf) rows per workgroup; NQK_LN_WPB = 1 / 2 / 4 (default 4)
+      const char* we = getenv("NQK_LN_WPB");
+      const int wpb = we && atoi(we) == 1 ? 1 : we && atoi(we) == 2 ? 2 : 4;
+      const int64_t rpw = wpb * 32 / p.nleaf;
       const unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
-#define LNL(NLV)                                                                                                   \
+#define LNL2(NLV, W)                                                                                               \
   if (mq)                                                                                                          \
-    hipLaunchKernelGGL((k_ln_quant_lds<NLV, true>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma,    \
-                       beta, out, rows, eps, scale, rs, (double)zp, lo, hi, lq);                                   \
+    hipLaunchKernelGGL((k_ln_quant_lds<NLV, true, W>), dim3(gl), dim3(64 * W), ln_lds_bytes(NLV, W), stream(), x,  \
+                       gamma, beta, out, rows, eps, scale, rs, (double)zp, lo, hi, lq);                            \
   else                                                                                                             \
-    hipLaunchKernelGGL((k_ln_quant_lds<NLV>), dim3(gl), dim3(256), ln_lds_bytes(NLV), stream(), x, gamma, beta,    \
-                       out, rows, eps, scale, rs, (double)zp, lo, hi, lq)
+    hipLaunchKernelGGL((k_ln_quant_lds<NLV, false, W>), dim3(gl), dim3(64 * W), ln_lds_bytes(NLV, W), stream(), x, \
+                       gamma, beta, out, rows, eps, scale, rs, (double)zp, lo, hi, lq)
+#define LNL(NLV)                \
+  if (wpb == 1) LNL2(NLV, 1);   \
+  else if (wpb == 2) LNL2(NLV, 2); \
+  else LNL2(NLV, 4)
       switch (p.nleaf) {
         case 8: LNL(8); break;
         case 4: LNL(4); break;
         default: LNL(2); break;
       }
+#undef LNL2
 #undef LNL
       return launch_status("nqk_ln_quant(lds)");
     }

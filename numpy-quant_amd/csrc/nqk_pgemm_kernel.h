@@ -445,7 +445,13 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     if constexpr ((NQK_PG_DIAG & 4) != 0) return;
     int8_t* st = lds + slot * STG;
     if (p < 2) {
-      if constexpr ((NQK_PG_DIAG & 256) == 0)  // (diagnostic 256: no A pieces, 128: no B pieces)
+      if constexpr ((NQK_PG_DIAG & 512) != 0) {
+        // (diagnostic 512, wrong values: the A piece as 8 rows x 128 B — whole cache lines, rows
+        // 8 (kt & 1) .. + 7 of the piece's 16 at the k-pair's 128-B block — the same bytes per step in
+        // half the L1 -> L2 requests)
+        const uint32_t v512 = (uint32_t)((32 * wave + 16 * p + 8 * (kt & 1) + (lane >> 3)) * lda + (lane & 7) * 16);
+        pg_dma16(r_a, st + (2 * wave + p) * 1024, v512, s.sa + (uint32_t)(kt & ~1) * PG_BK);
+      } else if constexpr ((NQK_PG_DIAG & 256) == 0)  // (diagnostic 256: no A pieces, 128: no B pieces)
         pg_dma16(r_a, st + (2 * wave + p) * 1024, va, s.sa + (uint32_t)p * 16u * (uint32_t)lda + kt * PG_BK);
     } else {
       if constexpr ((NQK_PG_DIAG & 128) == 0)

@@ -325,3 +325,31 @@ def test_ln_magic_quantize_equals_f64_chain(bw):
         got = (s.view(np.uint32) & 0xFF).astype(np.int64)
         got = np.where(got >= 128, got - 256, got)
         np.testing.assert_array_equal(got, ref, err_msg=f"zp {zp}")
+
+
+def test_ln_dma_swizzle_conflict_free():
+    """k_ln_quant_lds with NQK_LN_DMA (nqk_fused.hip ln_swz): the row image loaded by LDS-DMA is
+    XOR-swizzled so that the tree reads (lane (row, leaf, grp) reads 16-B chunk 24 leaf + 2 i + grp
+    of its row) put the 16 lanes of every ds_read_b128 lane group (MI355X_MICROARCH.md, LDS table)
+    on 16 different 4-bank slots, for 8, 4 and 2 leaves; the swizzle is a permutation of each row
+    that stays inside the leaf (its own inverse), so the loader can use it both ways."""
+    groups = [[0, 1, 2, 3, 12, 13, 14, 15] + list(range(20, 28)), list(range(4, 12)) + [16, 17, 18, 19] + list(range(28, 32))]
+    groups += [[g + 32 for g in grp] for grp in groups]
+
+    def swz(nl, r, c):  # nqk_fused.hip ln_swz
+        return c ^ (((((c // 24) >> 1) & 3) if nl == 8 else (r & 3)) << 1)
+
+    for nl in (8, 4, 2):
+        ch, lpr = 24 * nl, 2 * nl
+        for r in range(64 // lpr):
+            row = [swz(nl, r, c) for c in range(ch)]
+            assert sorted(row) == list(range(ch))
+            assert all(swz(nl, r, swz(nl, r, c)) == c and swz(nl, r, c) // 24 == c // 24 for c in range(ch))
+        for i in range(12):
+            for grp in groups:
+                slots = set()
+                for lane in grp:
+                    r, u = lane // lpr, lane % lpr
+                    leaf, g = u >> 1, u & 1
+                    slots.add((r * ch + swz(nl, r, 24 * leaf + 2 * i + g)) % 16)
+                assert len(slots) == 16, (nl, i, grp)

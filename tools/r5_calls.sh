@@ -154,4 +154,110 @@ r5_h() {
   echo done >> $STATUS
 }
 
+r5_i() {
+  # LayerNorm (k_ln_quant_lds): packed f32 pairs (NQK_LN_PK) and rows by LDS-DMA into a swizzled
+  # image (NQK_LN_DMA), both default on: parity, the kernel micro of all four builds (each checked
+  # byte for byte against the main build), then whole-bench A/B against the round-5 build (lnold)
+  rm -f $STATUS
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_fused_kernels.py tests/test_gpu_b256.py -x -q --timeout 300 \
+    --timeout-method thread > gpurun_out/i_tests.log 2>&1
+  step tests $?
+  LNM_LIBS=old=tools/diag/libnqk_lnold.so,pk=tools/diag/libnqk_lnpk.so,dma=tools/diag/libnqk_lndma.so LNM_ROUNDS=7 \
+    timeout -k 10 300 python -u tools/ln_micro.py > gpurun_out/i_ln_micro.txt 2>&1
+  step ln_micro $?
+  LNM_LIBS=old=tools/diag/libnqk_lnold.so LN_COLS=192 LNM_ROUNDS=7 timeout -k 10 300 python -u tools/ln_micro.py \
+    > gpurun_out/i_ln_micro_tiny.txt 2>&1
+  step ln_micro_tiny $?
+  AB_LIBS="main lnold" AB_REPS=3 OUT=i timeout -k 10 900 bash tools/ab.sh
+  step ab $?
+  echo done >> $STATUS
+}
+
+r5_j() {
+  # LayerNorm workgroup size (NQK_LN_WPB = 1 / 2 / 4 waves; LDS-DMA image for every leaf count):
+  # parity of the LN kernels at each size, then the kernel micro for ViT-Base and ViT-Ti rows
+  rm -f $STATUS
+  for w in 1 2 4; do
+    NQK_LN_WPB=$w timeout -k 10 300 python -u -m pytest tests/test_gpu_fused_kernels.py -k ln_quant -x -q --timeout 200 \
+      --timeout-method thread > gpurun_out/j_tests_w$w.log 2>&1
+    step tests_w$w $?
+  done
+  for c in 768 192; do
+    LNM_LIBS=old=tools/diag/libnqk_lnold.so LNM_ENV="w1:NQK_LN_WPB=1;w2:NQK_LN_WPB=2" LN_COLS=$c LNM_ROUNDS=7 \
+      timeout -k 10 300 python -u tools/ln_micro.py > gpurun_out/j_ln_micro_$c.txt 2>&1
+    step ln_micro_$c $?
+  done
+  echo done >> $STATUS
+}
+
+r5_k() {
+  # persistent double-buffered LayerNorm (NQK_LN_PERS = waves per CU) against the one-shot kernel at
+  # 4 and 1 waves per workgroup: parity at each, kernel micro for ViT-Base / ViT-Ti rows, then
+  # whole-bench A/B of both configs
+  rm -f $STATUS
+  for v in NQK_LN_PERS=6 NQK_LN_PERS=3 NQK_LN_WPB=1; do
+    env $v timeout -k 10 300 python -u -m pytest tests/test_gpu_fused_kernels.py -k ln_quant -x -q --timeout 200 \
+      --timeout-method thread > gpurun_out/k_tests_$v.log 2>&1
+    step tests_$v $?
+  done
+  for c in 768 192; do
+    LNM_ENV="w1:NQK_LN_WPB=1;p6:NQK_LN_PERS=6;p4:NQK_LN_PERS=4;p3:NQK_LN_PERS=3" LN_COLS=$c LNM_ROUNDS=7 \
+      timeout -k 10 300 python -u tools/ln_micro.py > gpurun_out/k_ln_micro_$c.txt 2>&1
+    step ln_micro_$c $?
+  done
+  for rep in 1 2; do
+    for cfg in vit vit_tiny; do
+      for v in main w1 p6; do
+        e=""; [ $v = w1 ] && e="NQK_LN_WPB=1"; [ $v = p6 ] && e="NQK_LN_PERS=6"
+        env $e timeout -k 10 300 python -u bench.py --config $cfg --no-cpu-baseline --no-secondary --steps 20 \
+          > gpurun_out/k_${cfg}_${v}_$rep.json 2> gpurun_out/k_${cfg}_${v}_$rep.err
+        step ${cfg}_${v} $?
+      done
+    done
+  done
+  echo done >> $STATUS
+}
+
+r5_l() {
+  # k_pg operand delivery: L1 -> L2 read requests and L2 reads / hits per projection shape (the A
+  # pieces read 64 of every 128-B line per k step), one --pmc pass per counter block
+  rm -f gpurun_out/l_pmc_*
+  for pass in tcp tcc; do
+    if [ $pass = tcp ]; then c="TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum"
+    else c="TCC_READ_sum TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum"; fi
+    PGM_ROUNDS=1 PGM_REPS=3 timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace -d gpurun_out/l_pmc_$pass -o run --output-format csv \
+      -- python -u tools/pg_micro.py > gpurun_out/l_pmc_$pass.log 2>&1
+    step pmc_$pass $?
+  done
+  echo done_l >> $STATUS
+}
+
+r5_m() {
+  # does k_pg's operand stream pay per L1 -> L2 request?  A pieces as whole 128-B lines (diagnostic
+  # 512: same bytes, half the A requests, wrong values) against the shipped pieces (16 rows x 64 B),
+  # with the full epilogue and without it (diagnostic 3 / 515), per-shape micro
+  rm -f $STATUS
+  PGM_LIBS=a512=tools/diag/libnqk_a512.so,d3=tools/diag/libnqk_d3.so,d3a=tools/diag/libnqk_d3a.so PGM_ROUNDS=3 \
+    timeout -k 10 400 python -u tools/pg_micro.py > gpurun_out/m_pg_micro.txt 2>&1
+  step pg_micro $?
+  echo done >> $STATUS
+}
+
+r5_n() {
+  # LayerNorm defaults: one-shot 4-wave workgroups (main), 1-wave workgroups (w1), persistent with 4
+  # waves per CU (p4), whole bench, 3 interleaved reps per config
+  rm -f $STATUS
+  for rep in 1 2 3; do
+    for cfg in vit vit_tiny; do
+      for v in main w1 p4; do
+        e=""; [ $v = w1 ] && e="NQK_LN_WPB=1"; [ $v = p4 ] && e="NQK_LN_PERS=4"
+        env $e timeout -k 10 300 python -u bench.py --config $cfg --no-cpu-baseline --no-secondary --steps 20 \
+          > gpurun_out/n_${cfg}_${v}_$rep.json 2> gpurun_out/n_${cfg}_${v}_$rep.err
+        step ${cfg}_${v} $?
+      done
+    done
+  done
+  echo done >> $STATUS
+}
+
 "r5_$1"
