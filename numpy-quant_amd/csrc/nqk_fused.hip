@@ -2328,9 +2328,11 @@ extern "C" int nqk_ln_quant(const float* x, const float* gamma, const float* bet
       return launch_status("nqk_ln_quant(pers)");
     }
     if (!getenv("NQK_LN_REG") && dma_ok) {
-      // WPB waves of 64 / (2 nleaf) rows per workgroup; NQK_LN_WPB = 1 / 2 / 4 (default 4)
+      // WPB waves of 64 / (2 nleaf) rows per workgroup; NQK_LN_WPB = 1 / 2 / 4 (default: 4 for 8 leaves,
+      // 1 for fewer — ViT-Ti's 192-column rows +1.3 % whole-bench, ViT-Base's -0.5 %, within noise:
+      // profiles/r05_ln_variants.txt)
       const char* we = getenv("NQK_LN_WPB");
-      const int wpb = we && atoi(we) == 1 ? 1 : we && atoi(we) == 2 ? 2 : 4;
+      const int wpb = we ? (atoi(we) == 1 ? 1 : atoi(we) == 2 ? 2 : 4) : (p.nleaf == 8 ? 4 : 1);
       const int64_t rpw = wpb * 32 / p.nleaf;
       const unsigned gl = (unsigned)((rows + rpw - 1) / rpw);
 #define LNL2(NLV, W)                                                                                               \

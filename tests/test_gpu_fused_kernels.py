@@ -43,6 +43,31 @@ def test_ln_quant(rows, cols, bw, zp, path, monkeypatch):
     np.testing.assert_array_equal(out.to_host().astype(np.int64), ref)
 
 
+@pytest.mark.parametrize("rows,cols", [(4109, 768), (40000, 192), (9001, 384)])
+@pytest.mark.parametrize("variant", ["NQK_LN_WPB=1", "NQK_LN_WPB=2", "NQK_LN_WPB=4", "NQK_LN_PERS=1", "NQK_LN_PERS=4",
+                                     "NQK_LN_PERS=6"])
+def test_ln_quant_workgroup_forms_match_oracle(rows, cols, variant, monkeypatch):
+    """Every launch form of the LDS LayerNorm (nqk_fused.hip: 1 / 2 / 4 row groups per workgroup;
+    the persistent double-buffered k_ln_quant_pers at 1 / 4 / 6 waves per CU, whose waves walk
+    many row groups with the next group's LDS-DMA in flight — 40 000 x 192 at one wave per CU is
+    ~10 groups per wave; ragged last groups) against the oracle, bit for bit."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    monkeypatch.delenv("NQK_LN_REG", raising=False)
+    k, v = variant.split("=")
+    monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(rows + cols)
+    x = (rng.standard_normal((rows, cols)) * 3 - 0.7).astype(np.float32)
+    g = (1 + 0.05 * rng.standard_normal(cols)).astype(np.float32)
+    b = (0.05 * rng.standard_normal(cols)).astype(np.float32)
+    s, zp = np.float32(0.0021), 5
+    dx, dg, db = DeviceArray.from_host(x), DeviceArray.from_host(g), DeviceArray.from_host(b)
+    out = DeviceArray((rows, cols), np.int8)
+    _lib.call("nqk_ln_quant", dx.vp, dg.vp, db.vp, out.vp, rows, cols, 1e-5, float(s), zp, 8)
+    ref = O.quantize(_ln_ref(x, g, b, np.float32(1e-5)), 8, s, np.int64(zp))
+    np.testing.assert_array_equal(out.to_host().astype(np.int64), ref)
+
+
 @pytest.mark.parametrize("s,zp,bw", [(0.031, -3, 8), (0.0021, 5, 8), (0.0007, -120, 8), (0.45, 1, 4), (0.031, 1 << 20, 8)])
 def test_ln_quant_lds_small_scales_match_oracle(s, zp, bw, monkeypatch):
     """The LDS LayerNorm + quantize on ViT-Base rows (4109 x 768: a ragged last workgroup)
