@@ -78,6 +78,9 @@ int nqk_event_create(void** event);
 int nqk_event_record(void* event);
 int nqk_event_elapsed(void* start, void* stop, float* ms);   /* waits for stop */
 int nqk_event_destroy(void* event);
+/* the current stream waits for the work an event recorded (cross-stream ordering of the fused
+ * plan's batch parts: NQK_STREAM_LAG) */
+int nqk_event_wait(void* event);
 /* hipGraph capture of everything issued between begin and end (relaxed mode: the
  * caller's allocator may still allocate); abort drops a capture that failed part-way */
 int nqk_graph_begin(void);

@@ -185,7 +185,10 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   }
   const int tiles_n = (int)((N + PG_BN - 1) / PG_BN), tiles_m = (int)((M + wm * PG_BM - 1) / (wm * PG_BM));
   const int nt = tiles_m * tiles_n;
-  const int slots = (wm == 2 ? 1 : 2) * pg_num_cus();
+  // NQK_PG_WGPC=1: one workgroup per CU (the other half of the register file free for the other
+  // stream's kernels: A/B switch with NQK_STREAM_LAG)
+  const char* wgpc = getenv("NQK_PG_WGPC");
+  const int slots = (wm == 2 || (wgpc && atoi(wgpc) == 1) ? 1 : 2) * pg_num_cus();
   const int kc = K == 3072 ? 2 : (K == 192 ? 1 : 0);
   const int epi_k = glut ? PG_GLUT : epi;
   const bool s8 = epi == PG_QKV && p->bit_width == 8 && !b4 && !getenv("NQK_PG_NOS8");

@@ -141,6 +141,7 @@ int nqk_event_elapsed(void* start, void* stop, float* ms) {
   return check(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop), "hipEventElapsedTime");
 }
 int nqk_event_destroy(void* event) { return check(hipEventDestroy((hipEvent_t)event), "hipEventDestroy"); }
+int nqk_event_wait(void* event) { return check(hipStreamWaitEvent(stream(), (hipEvent_t)event, 0), "hipStreamWaitEvent"); }
 
 int nqk_graph_begin(void) {
   // relaxed: the caching allocator may still hipMalloc a fresh block mid-capture

@@ -69,6 +69,7 @@ SIGNATURES = {
     "nqk_event_record": [_p],
     "nqk_event_elapsed": [_p, _p, ctypes.POINTER(_f)],
     "nqk_event_destroy": [_p],
+    "nqk_event_wait": [_p],
     "nqk_graph_begin": [],
     "nqk_graph_end": [ctypes.POINTER(_p)],
     "nqk_graph_abort": [],

@@ -96,6 +96,24 @@ class Streams:
 _ONE_STREAM = Streams(False)
 
 
+def _stream_lag():
+    v = os.environ.get("NQK_STREAM_LAG", "")
+    return v if v in ("ln1", "qkv", "attn") else None
+
+
+_LAG_EVENTS = {}
+
+
+def _lag_event(i):
+    """The event part i records at its NQK_STREAM_LAG point (one per part, reused every layer:
+    part i + 1 waits for it right after part i's layer is issued)."""
+    if i not in _LAG_EVENTS:
+        e = ctypes.c_void_p()
+        _lib.call("nqk_event_create", ctypes.byref(e))
+        _LAG_EVENTS[i] = e
+    return _LAG_EVENTS[i]
+
+
 def embed_q_fits(images: int, hw: int, kout: int) -> bool:
     """Whether one nqk_embed_q call over `images` images of hw patches takes the shape: at most
     65535 row tiles of 128 patches, and (images x (hw + 1)) x kout < 2^31 (its 32-bit output
@@ -680,12 +698,21 @@ class FusedLayer:
         if not self.attn_fused:
             streams.join()  # the three-launch attention runs whole-batch on stream 0
             streams = _ONE_STREAM
-        streams.halves(B, lambda s_idx, i0, nb: self._run_part(w, x.dev, w["x1"], x2, i0, nb))
+        streams.halves(B, lambda s_idx, i0, nb: self._run_part(w, x.dev, w["x1"], x2, i0, nb, s_idx, streams.parts))
         m.x_out.data = FTensor(x2)
 
-    def _run_part(self, w, xd, x1d, x2d, i0, nb):
-        """Images [i0, i0 + nb) of the layer (row views of every buffer)."""
+    def _run_part(self, w, xd, x1d, x2d, i0, nb, s_idx=0, parts=1):
+        """Images [i0, i0 + nb) of the layer (row views of every buffer).  NQK_STREAM_LAG
+        (ln1 / qkv / attn): part s > 0 starts the layer only after part s - 1 has finished that
+        kernel of it, so the parts' kernels of different kinds run side by side (A/B switch)."""
         m, bw = self.m, self.bw
+        lag = _stream_lag() if parts > 1 else None
+        if lag and s_idx > 0:
+            _lib.call("nqk_event_wait", _lag_event(s_idx - 1))
+
+        def mark(point):
+            if lag == point and s_idx + 1 < parts:
+                _lib.call("nqk_event_record", _lag_event(s_idx))
         T, D = m.tokens, self.D
         H, Dh, F = m.heads, m.hdim, self.F
         Mrows = nb * T
@@ -702,6 +729,7 @@ class FusedLayer:
         call = _lib.call
         # 1) LN1 + quantize (LN1 output feeds the Q/K/V MatMuls)
         _ln_quant(x, self.g1, self.be1, lnq, Mrows, D, self.eps1, self.p_ln1, bw)
+        mark("ln1")
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln1), group_cols=D, col=self.col_qkv.ptr,
@@ -711,6 +739,7 @@ class FusedLayer:
                       zp_out=[_zp(self.p_head[r]) for r in "qkv"],
                       out=[q.ptr, k.ptr, v.ptr], bias=self.bias_qkv.ptr)
         _gemm(EPI_QKV, lnq, self._b(e, "qkv", self.bt_qkv), 1, Mrows, 3 * D, D, D, D, None, 0, 0, e)
+        mark("qkv")
         pq, pk, pv_ = self.p_head["q"], self.p_head["k"], self.p_head["v"]
         if self.attn_fused:
             # 3-6) one kernel per (image, head): scores, softmax, P V, context quantize
@@ -727,6 +756,7 @@ class FusedLayer:
                 KM.TIMER.end("attention", t0, (2 * 2 * nb * H * T * T * Dh, 3 * nb * H * T * Dh + nb * T * D))
         else:
             self._attention_unfused(w, nb, T, Tp, H, Dh, D)  # whole batch only (i0 == 0)
+        mark("attn")
         # 7) output projection + bias + residual
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ctx), col=self.col_o.ptr, col_absmax=self.cmax["o"], col_l1max=self.l1max["o"],
                       colterm=_ptr(self.ct["o"]),

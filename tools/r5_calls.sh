@@ -260,4 +260,28 @@ r5_n() {
   echo done >> $STATUS
 }
 
+r5_o() {
+  # the two batch parts offset so that different kernel kinds run side by side (NQK_STREAM_LAG: part
+  # 1 starts a layer after part 0's LN1 / QKV / attention), with k_pg at one workgroup per CU
+  # (NQK_PG_WGPC=1: half the register file left for the other part's attention), whole bench
+  rm -f $STATUS
+  timeout -k 10 300 env NQK_STREAM_LAG=qkv NQK_PG_WGPC=1 python -u -m pytest tests/test_gpu_b256.py -x -q --timeout 200 \
+    --timeout-method thread > gpurun_out/o_tests.log 2>&1
+  step tests $?
+  for rep in 1 2; do
+    for v in main lagqkv lagattn lagln1 wgpc1 lagqkv_wgpc1 lagattn_wgpc1; do
+      e=""
+      case $v in
+        lagqkv) e="NQK_STREAM_LAG=qkv";; lagattn) e="NQK_STREAM_LAG=attn";; lagln1) e="NQK_STREAM_LAG=ln1";;
+        wgpc1) e="NQK_PG_WGPC=1";; lagqkv_wgpc1) e="NQK_STREAM_LAG=qkv NQK_PG_WGPC=1";;
+        lagattn_wgpc1) e="NQK_STREAM_LAG=attn NQK_PG_WGPC=1";;
+      esac
+      env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-secondary --steps 20 \
+        > gpurun_out/o_${v}_$rep.json 2> gpurun_out/o_${v}_$rep.err
+      step ${v}_$rep $?
+    done
+  done
+  echo done >> $STATUS
+}
+
 "r5_$1"
