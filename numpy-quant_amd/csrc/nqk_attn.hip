@@ -148,6 +148,24 @@ __device__ __forceinline__ float xor32f(float x) { return __int_as_float(xor32i(
 #ifndef NQK_ATTN_MINB
 #define NQK_ATTN_MINB 3
 #endif
+#ifndef NQK_ATTN_TAIL
+#define NQK_ATTN_TAIL 0  // 1: the last row tile of T = 193 .. 200 by the row-parallel path (round 5; measured no faster,
+                         // profiles/r05_attn_tail_dropped.txt: opt-in build)
+#endif
+constexpr int ATTN_TSTR = 232;
+// the row-parallel tail path applies: the shipped FAST configuration, T > 128 with at most 8 real
+// rows in the last tile and both pairwise-sum leaves of equal group counts (T = 193 .. 200)
+template <int NT, int TC, bool FAST>
+constexpr bool attn_tail() {
+  constexpr int TR = TC > 0 ? TC - 32 * (NT - 1) : 32;
+  constexpr int N2 = TC > 128 ? TC / 2 - (TC / 2) % 8 : 0;
+  return NQK_ATTN_TAIL && FAST && NQK_ATTN_PK && NQK_ATTN_EXP2 && NQK_ATTN_PQ2 && NQK_ATTN_PREL && !NQK_ATTN_PKL &&
+         NQK_ATTN_DIAG == 0 && TC > 128 && TR >= 1 && TR <= 8 && N2 / 8 == (TC - N2) / 8;
+}
+template <int NT, int TC, bool FAST>
+constexpr size_t attn_tail_lds() {
+  return attn_tail<NT, TC, FAST>() ? (size_t)(TC - 32 * (NT - 1)) * (ATTN_TSTR * 4 + NT * 32) : 0;
+}
 template <int NT, int TC, bool FAST>  // TC: compile-time token count (0: runtime a.T)
 __global__ void __launch_bounds__(256, NQK_ATTN_MINB) NQK_ATTN_OCC
 k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int8_t* __restrict__ Vg,
@@ -157,6 +175,13 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   // group qq of score tile c (columns c*32 + 8qq .. + 7 of both halves) past the last
   // token: known at compile time when the token count is
   auto pad_group = [](int c, int qq) constexpr { return TC > 0 && c * 32 + 8 * qq >= TC; };
+  // NQK_ATTN_TAIL: the last row tile's TR real rows by the row-parallel path (below); its LDS: the
+  // rows' scores tS [TR][TSTR] f32 (rows 8 banks apart for ds_read_b32) and P bytes tP [TR][TP]
+  constexpr int TR = TC > 0 ? TC - 32 * (NT - 1) : 32;
+  constexpr int N2 = TC > 128 ? TC / 2 - (TC / 2) % 8 : 0, NG0 = N2 / 8, NG1 = (TC - N2) / 8, NG = NG0 + NG1;
+  constexpr int TL1 = TC - N2 - 8 * NG1;
+  constexpr bool TAILR = attn_tail<NT, TC, FAST>();
+  constexpr int TSTR = ATTN_TSTR;
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int T = TC ? TC : a.T, PST = TC ? NT * 32 + 16 : a.PST;
   int8_t* Ks = lds;
@@ -164,6 +189,8 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   auto vt_row = [&](int d) { return d * PST + (d >> 4) * 64; };  // byte offset of V^T row d
   int* colK = reinterpret_cast<int*>(Vt + 64 * PST + 256);  // rowsum(K[n]) * zq - zq*zk*64
   int* colV = colK + TP;                              // colsum(V[:, d]) * zp - zp*zv*T
+  float* const tS = reinterpret_cast<float*>(colV + 64);  // NQK_ATTN_TAIL scratch
+  int8_t* const tP = reinterpret_cast<int8_t*>(tS + (TAILR ? TR * TSTR : 0));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x;
   const int img = bh / a.H, head = bh - img * a.H;
@@ -236,27 +263,94 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   const int r32 = lane & 31, h = lane >> 5;
   // (NT = 7 row tiles on 4 waves: wave 3 holds one.  Rotating that light wave over the
   // waves by blockIdx measured 2 % slower, profiles/r04_attn_variants_ab.txt)
-  for (int rt = wave; rt < NT; rt += 4) {
+  // per row tile: the lane's query row m (clamped to the last token): Q fragments and minus the row term
+  auto q_rows = [&](int m, v4i (&qb)[2]) __attribute__((always_inline)) {
+      {
+        // (Q rows by LDS-DMA at the workgroup's start instead: no faster on the bench's data,
+        // profiles/r04_attn_real_data.txt)
+        const int qrow = min(m, T - 1);
+        if constexpr ((NQK_ATTN_DIAG & 2048) != 0) {  // (diagnostic 2048: Q rows from the LDS K image, no Q loads)
+          qb[0] = *reinterpret_cast<const v4i*>(Ks + swz64a(qrow, h));
+          qb[1] = *reinterpret_cast<const v4i*>(Ks + swz64a(qrow, 2 + h));
+        } else {
+          qb[0] = *reinterpret_cast<const v4i*>(q + qrow * 64 + h * 16);
+          qb[1] = *reinterpret_cast<const v4i*>(q + qrow * 64 + (2 + h) * 16);
+        }
+      }
+      int rq = sum16a(qb[0]) + sum16a(qb[1]);
+      rq += xor32i(rq);
+      // minus the row term: acc init = nrowterm - colterm, one v_sub per element (the empty asm
+      // keeps the compiler from re-associating it into -(rowterm + colterm): an add and a sub)
+      int nrowterm = -(rq * a.zk);
+      asm volatile("" : "+v"(nrowterm));
+    return nrowterm;
+  };
+  // dequant + quantize (EPI_PV) of a row tile's context -> ctx[img][m][head * 64 + d], 4 dims per store
+  auto ctx_store = [&](int m, int rp, const v16i (&acc2)[2]) __attribute__((always_inline)) {
+    const int rowp = rp * a.zv;
+    int8_t* orow = ctx + ((int64_t)img * T + m) * a.ld_out + head * 64;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int d0 = j * 32 + 8 * qq + 4 * h;
+        const v4i cv = *reinterpret_cast<const v4i*>(colV + d0);
+        uint32_t packed = 0;
+        int qs[4];
+        float o[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int vv = acc2[j][4 * qq + jj] - rowp - cv[jj];
+          o[jj] = FAST ? (float)vv * a.s_pv : (float)((double)vv * (double)a.s_pv);
+        }
+        if constexpr ((NQK_ATTN_DIAG & 16) != 0) {  // (diagnostic 16: context bytes without the quantize)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) qs[jj] = (int)o[jj];
+        } else if constexpr (FAST) {
+          // rint(zp + t) for t = RN(o / s_ctx) approximated by tf = o rs (|t - tf| <= |tf| 2^-21),
+          // on pairs: one v_pk_mul, clamp + magic-number rounding (round_magic2), and the
+          // measure |tf| 2^-21 + |dd| of the four elements: below 0.5 - 2^-23 every element's
+          // rounding boundary is farther than the error, else the exact chain (quant_w)
+          v2f_t dd0, dd1;
+          const v2f_t t0 = v2f_t{o[0], o[1]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
+          const v2f_t t1 = v2f_t{o[2], o[3]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
+          const v2f_t s0 = round_magic2(t0, a.lo_f - a.zp_ctx_f, a.hi_f - a.zp_ctx_f, 0x1.8p23f + a.zp_ctx_f, dd0);
+          const v2f_t s1 = round_magic2(t1, a.lo_f - a.zp_ctx_f, a.hi_f - a.zp_ctx_f, 0x1.8p23f + a.zp_ctx_f, dd1);
+          const float m0 = __builtin_fmaf(__builtin_fabsf(t0[0]), 0x1p-21f, __builtin_fabsf(dd0[0]));
+          const float m1 = __builtin_fmaf(__builtin_fabsf(t0[1]), 0x1p-21f, __builtin_fabsf(dd0[1]));
+          const float m2 = __builtin_fmaf(__builtin_fabsf(t1[0]), 0x1p-21f, __builtin_fabsf(dd1[0]));
+          const float m3 = __builtin_fmaf(__builtin_fabsf(t1[1]), 0x1p-21f, __builtin_fabsf(dd1[1]));
+          // NaN / inf order above every finite measure as unsigned bits
+          const uint32_t wm = __builtin_elementwise_max(__builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)),
+                                                        __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3)));
+          packed = pack4_low(s0, s1);
+          if (__builtin_expect(__any(wm >= __float_as_uint(0x1.fffffcp-2f)), 0)) {
+            NQK_ATTN_COUNT(3);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int qv = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
+              packed = (packed & ~(0xffu << (8 * jj))) | ((uint32_t)(qv & 0xff) << (8 * jj));
+            }
+          }
+          if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
+          __builtin_amdgcn_sched_barrier(0);
+          continue;
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) qs[jj] = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) packed |= ((uint32_t)(qs[jj] & 0xff)) << (8 * jj);
+        if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  };
+  for (int rt = wave; rt < (TAILR ? NT - 1 : NT); rt += 4) {
     const int m0 = rt * 32, m = m0 + r32;
     v4i qb[2];
-    {
-      // (Q rows by LDS-DMA at the workgroup's start instead: no faster on the bench's data,
-      // profiles/r04_attn_real_data.txt)
-      const int qrow = min(m, T - 1);
-      if constexpr ((NQK_ATTN_DIAG & 2048) != 0) {  // (diagnostic 2048: Q rows from the LDS K image, no Q loads)
-        qb[0] = *reinterpret_cast<const v4i*>(Ks + swz64a(qrow, h));
-        qb[1] = *reinterpret_cast<const v4i*>(Ks + swz64a(qrow, 2 + h));
-      } else {
-        qb[0] = *reinterpret_cast<const v4i*>(q + qrow * 64 + h * 16);
-        qb[1] = *reinterpret_cast<const v4i*>(q + qrow * 64 + (2 + h) * 16);
-      }
-    }
-    int rq = sum16a(qb[0]) + sum16a(qb[1]);
-    rq += xor32i(rq);
-    // minus the row term: acc init = nrowterm - colterm, one v_sub per element (the empty asm
-    // keeps the compiler from re-associating it into -(rowterm + colterm): an add and a sub)
-    int nrowterm = -(rq * a.zk);
-    asm volatile("" : "+v"(nrowterm));
+    const int nrowterm = q_rows(m, qb);
+    int rp;
+    v16i acc2[2];
     // ---- per score tile c: S^T = K Q^T (two MFMAs), dequant + Div (EPI_SCORES), row
     // max; only one tile's accumulators are live
     float e[NT][16];
@@ -479,7 +573,7 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     // ---- per score tile c: P = quantize(e / tot) (4 packed bytes per group, row sums),
     // then at once its share of O^T = V^T P^T (B operand = P row m, 16 consecutive tokens
     // per half), so only one tile's packed P is live
-    int rp = 0;
+    rp = 0;
     // NQK_ATTN_PQ2: when every lane's kpf <= pqhi (and pqlo <= 0), e kpf in [0, kpf] never
     // reaches a clamp (wave-uniform): s = RN(e kpf + pmagic) is rint(e kpf) + pmagic from
     // the exact product (one rounding fewer than tf = RN(e kpf), so still within |t| 2^-22 of
@@ -489,7 +583,6 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
     const bool pq_nc = NQK_ATTN_PQ2 && ((NQK_ATTN_DIAG & 512) != 0 || (pqlo <= 0.0f && __all(kpf <= pqhi)));
     const float plim2 = plim - 0x1p-24f;
     if (!pq_nc) NQK_ATTN_COUNT(1);
-    v16i acc2[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -680,64 +773,199 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
       }
     }
     rp += xor32i(rp);
-    // ---- dequant + quantize (EPI_PV) -> ctx[img][m][head * 64 + d], 4 dims per store
-    const int rowp = rp * a.zv;
-    int8_t* orow = ctx + ((int64_t)img * T + m) * a.ld_out + head * 64;
+    ctx_store(m, rp, acc2);
+  }
+  if constexpr (TAILR) {
+    if (wave == (NT - 1) % 4) {
+      const int rt = NT - 1, m = rt * 32 + r32;
+      v4i qb[2];
+      const int nrowterm = q_rows(m, qb);
+      int rp;
+      v16i acc2[2];
+      // ---- the last row tile (NQK_ATTN_TAIL): TR real query rows of 32.  The scores of those
+      // rows go to LDS, and the softmax / P quantize run with one lane per (row, NumPy
+      // accumulator n % 8) — NG + 1 elements a lane instead of 112 — then P comes back to the
+      // MFMA layout for P V.  Same operations per element as the full tile, the pairwise sum's
+      // accumulator chains and combination tree unchanged (every add of the tree is commutative).
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int c = 0; c < NT; ++c) {
+        v16i acc;
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int d0 = j * 32 + 8 * qq + 4 * h;
-        const v4i cv = *reinterpret_cast<const v4i*>(colV + d0);
-        uint32_t packed = 0;
-        int qs[4];
-        float o[4];
+        for (int qq = 0; qq < 4; ++qq) {
+          if (pad_group(c, qq)) {
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int vv = acc2[j][4 * qq + jj] - rowp - cv[jj];
-          o[jj] = FAST ? (float)vv * a.s_pv : (float)((double)vv * (double)a.s_pv);
-        }
-        if constexpr ((NQK_ATTN_DIAG & 16) != 0) {  // (diagnostic 16: context bytes without the quantize)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) qs[jj] = (int)o[jj];
-        } else if constexpr (FAST) {
-          // rint(zp + t) for t = RN(o / s_ctx) approximated by tf = o rs (|t - tf| <= |tf| 2^-21),
-          // on pairs: one v_pk_mul, clamp + magic-number rounding (round_magic2), and the
-          // measure |tf| 2^-21 + |dd| of the four elements: below 0.5 - 2^-23 every element's
-          // rounding boundary is farther than the error, else the exact chain (quant_w)
-          v2f_t dd0, dd1;
-          const v2f_t t0 = v2f_t{o[0], o[1]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
-          const v2f_t t1 = v2f_t{o[2], o[3]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
-          const v2f_t s0 = round_magic2(t0, a.lo_f - a.zp_ctx_f, a.hi_f - a.zp_ctx_f, 0x1.8p23f + a.zp_ctx_f, dd0);
-          const v2f_t s1 = round_magic2(t1, a.lo_f - a.zp_ctx_f, a.hi_f - a.zp_ctx_f, 0x1.8p23f + a.zp_ctx_f, dd1);
-          const float m0 = __builtin_fmaf(__builtin_fabsf(t0[0]), 0x1p-21f, __builtin_fabsf(dd0[0]));
-          const float m1 = __builtin_fmaf(__builtin_fabsf(t0[1]), 0x1p-21f, __builtin_fabsf(dd0[1]));
-          const float m2 = __builtin_fmaf(__builtin_fabsf(t1[0]), 0x1p-21f, __builtin_fabsf(dd1[0]));
-          const float m3 = __builtin_fmaf(__builtin_fabsf(t1[1]), 0x1p-21f, __builtin_fabsf(dd1[1]));
-          // NaN / inf order above every finite measure as unsigned bits
-          const uint32_t wm = __builtin_elementwise_max(__builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)),
-                                                        __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3)));
-          packed = pack4_low(s0, s1);
-          if (__builtin_expect(__any(wm >= __float_as_uint(0x1.fffffcp-2f)), 0)) {
-            NQK_ATTN_COUNT(3);
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              const int qv = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
-              packed = (packed & ~(0xffu << (8 * jj))) | ((uint32_t)(qv & 0xff) << (8 * jj));
-            }
+            for (int j = 0; j < 4; ++j) acc[4 * qq + j] = 0;
+            continue;
           }
-          if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
-          __builtin_amdgcn_sched_barrier(0);
-          continue;
-        } else {
+          const v4i ck = *reinterpret_cast<const v4i*>(colK + c * 32 + 8 * qq + 4 * h);
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) qs[jj] = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
+          for (int j = 0; j < 4; ++j) acc[4 * qq + j] = nrowterm - ck[j];
         }
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) packed |= ((uint32_t)(qs[jj] & 0xff)) << (8 * jj);
-        if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
-        __builtin_amdgcn_sched_barrier(0);
+        for (int s = 0; s < 2; ++s) {
+          const v4i ka = *reinterpret_cast<const v4i*>(Ks + swz64a(c * 32 + r32, 2 * s + h));
+          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(ka, qb[s], acc, 0, 0, 0);
+        }
+        if (r32 < TR) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            if (pad_group(c, qq)) continue;
+            const v2f_t y01 = v2f_t{(float)acc[4 * qq], (float)acc[4 * qq + 1]} * v2f_t{a.s_qkd, a.s_qkd};
+            const v2f_t y23 = v2f_t{(float)acc[4 * qq + 2], (float)acc[4 * qq + 3]} * v2f_t{a.s_qkd, a.s_qkd};
+            *reinterpret_cast<float4*>(tS + r32 * TSTR + c * 32 + 8 * qq + 4 * h) = make_float4(y01[0], y01[1], y23[0], y23[1]);
+          }
+        }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      // lane (ti, tj): row ti (rows >= TR mirror row TR - 1: computed, never stored), elements
+      // n = 8 g + tj (g < NG: NG0 groups of leaf 0, NG1 of leaf 1) and the tail element 8 NG + tj
+      const int ti = min(lane >> 3, TR - 1), tj = lane & 7, tb = lane & ~7;
+      const bool real = (lane >> 3) < TR;
+      float* const srow = tS + ti * TSTR;
+      // (streamed through LDS in three passes, so the path holds no per-element registers: the
+      // kernel's full tiles keep their register budget)
+      const float xt = tj < TL1 ? srow[8 * NG + tj] : -__builtin_inff();
+      float mxl = xt, mnl = tj < TL1 ? xt : __builtin_inff();
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const float v = srow[8 * g + tj];
+        mxl = __builtin_fmaxf(mxl, v), mnl = __builtin_fminf(mnl, v);
+      }
+#pragma unroll
+      for (int sh = 1; sh < 8; sh <<= 1) {
+        mxl = __builtin_fmaxf(mxl, __shfl_xor(mxl, sh, 64));
+        mnl = __builtin_fminf(mnl, __shfl_xor(mnl, sh, 64));
+      }
+      const float nm = -mxl;
+      const bool esafe = __all(mnl + nm >= NP_EXP_SAFE_LO);
+      // exp of elements g (leaf 0) and NG0 + g (leaf 1) as a pair, written back over the scores;
+      // NumPy's pairwise sum: accumulator tj of each leaf in increasing n (the pair's lanes), the
+      // 8 accumulators of a leaf combined ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) by xor
+      // butterflies, leaf 1's tail elements added in order, then leaf 0 + leaf 1
+      v2f_t ls;
+#pragma unroll
+      for (int g = 0; g < NG0; ++g) {
+        const v2f_t xa = v2f_t{srow[8 * g + tj], srow[8 * (NG0 + g) + tj]} + v2f_t{nm, nm};
+        const v2f_t ex = esafe ? np_expf_safe2(xa) : np_expf_nonpos2(xa);
+        ls = g == 0 ? ex : ls + ex;
+        if (real) srow[8 * g + tj] = ex[0], srow[8 * (NG0 + g) + tj] = ex[1];
+      }
+      const float et = np_expf_nonpos2(v2f_t{xt + nm, xt + nm})[0];  // (no tail element: -inf -> 0)
+#pragma unroll
+      for (int sh = 1; sh < 8; sh <<= 1) ls = ls + v2f_t{__shfl_xor(ls[0], sh, 64), __shfl_xor(ls[1], sh, 64)};
+      float leaf1 = ls[1];
+#pragma unroll
+      for (int t = 0; t < TL1; ++t) leaf1 = leaf1 + __shfl(et, tb + t, 64);
+      const float tot = ls[0] + leaf1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const double rtot = 1.0 / (double)tot;
+      const float kpf = (float)(rtot * a.rs_p);
+      const float pqlo = a.lo_f - a.zp_p_f, pqhi = a.hi_f - a.zp_p_f, pmagic = 0x1.8p23f + a.zp_p_f;
+      const bool pq_nc = pqlo <= 0.0f && __all(kpf <= pqhi);
+      // P = quantize(e / tot) by the full tile's filtered fast path, exact chain where it cannot decide
+      const v2f_t k2 = v2f_t{kpf, kpf}, m2 = v2f_t{pmagic, pmagic};
+      constexpr int NPW = (NG + 4) / 4;
+      uint32_t pw[NPW];  // the lane's P bytes, 4 to a word: element g in byte g % 4 of word g / 4
+#pragma unroll
+      for (int w = 0; w < NPW; ++w) pw[w] = 0u;
+      auto put = [&](int g, int q) __attribute__((always_inline)) {
+        pw[g >> 2] = (pw[g >> 2] & ~(0xffu << (8 * (g & 3)))) | ((uint32_t)(q & 0xff) << (8 * (g & 3)));
+      };
+      auto get = [&](int g) __attribute__((always_inline)) { return (int)(int8_t)(pw[g >> 2] >> (8 * (g & 3))); };
+      uint32_t fails = 0;
+      auto quant_pair = [&](v2f_t e2, int& q0, int& q1, uint32_t& f0, uint32_t& f1) __attribute__((always_inline)) {
+        v2f_t s2, dd, mag;
+        if (pq_nc) {
+          s2 = __builtin_elementwise_fma(e2, k2, m2);
+          const v2f_t r2 = s2 - m2;
+          dd = __builtin_elementwise_fma(e2, k2, -r2);
+          mag = r2;
+        } else {
+          const v2f_t tf = e2 * k2;
+          s2 = round_magic2(tf, pqlo, pqhi, pmagic, dd);
+          mag = tf;
+        }
+        const float mr = pq_nc ? NQK_ATTN_PM_R : NQK_ATTN_PM_T;
+        f0 = !(__builtin_fmaf(__builtin_fabsf(mag[0]), mr, __builtin_fabsf(dd[0])) < 0x1.fffff8p-2f);
+        f1 = !(__builtin_fmaf(__builtin_fabsf(mag[1]), mr, __builtin_fabsf(dd[1])) < 0x1.fffff8p-2f);
+        q0 = (int)(int8_t)(__float_as_uint(s2[0]) & 0xffu);
+        q1 = (int)(int8_t)(__float_as_uint(s2[1]) & 0xffu);
+      };
+#pragma unroll
+      for (int g = 0; g < NG; g += 2) {
+        uint32_t f0, f1;
+        int q0, q1;
+        quant_pair(v2f_t{srow[8 * g + tj], srow[8 * (g + 1) + tj]}, q0, q1, f0, f1);
+        put(g, q0);
+        put(g + 1, q1);
+        fails |= (f0 << g) | (f1 << (g + 1));
+      }
+      {
+        uint32_t f0, f1;
+        int q0, qd;
+        quant_pair(v2f_t{et, et}, q0, qd, f0, f1);
+        put(NG, tj < TL1 ? q0 : 0);  // (no tail element: 0, so the byte sum below needs no mask)
+        fails |= (tj < TL1 ? f0 : 0u) << NG;
+      }
+      if (__builtin_expect(__any(fails != 0), 0)) {
+        NQK_ATTN_COUNT(2);
+#pragma unroll
+        for (int g = 0; g <= NG; ++g)
+          if ((fails >> g) & 1u) put(g, quant_w(div_rc_w(g < NG ? srow[8 * g + tj] : et, rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi));
+      }
+      int rps = 0;
+#pragma unroll
+      for (int w = 0; w < NPW; ++w) rps = __builtin_amdgcn_sdot4((int)pw[w], 0x01010101, rps, false);  // signed bytes
+#pragma unroll
+      for (int sh = 1; sh < 8; sh <<= 1) rps += __shfl_xor(rps, sh, 64);
+      if ((lane >> 3) < TR) {
+        int8_t* prow = tP + (lane >> 3) * TP;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) prow[8 * g + tj] = (int8_t)get(g);
+        if (tj < TL1) prow[8 * NG + tj] = (int8_t)get(NG);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      // ---- P back in the MFMA layout (rows >= TR and columns >= T: 0), then P V as the full tile
+      rp = __shfl(rps, min(r32, TR - 1) * 8, 64);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[j][r] = 0;
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        int dw[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          if (pad_group(c, qq)) {
+            dw[qq] = 0;
+            continue;
+          }
+          const int n = c * 32 + 8 * qq + 4 * h;
+          uint32_t w = r32 < TR ? *reinterpret_cast<const uint32_t*>(tP + r32 * TP + n) : 0u;
+          if (!(c * 32 + 8 * qq + 8 <= TC)) {
+            uint32_t keep = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) keep |= (n + j < T ? 0xffu : 0u) << (8 * j);
+            w &= keep;
+          }
+          dw[qq] = (int)w;
+        }
+        const int xa = xor32i(h ? dw[0] : dw[2]);
+        const int xb = xor32i(h ? dw[1] : dw[3]);
+        v4i pb;
+        if (h) { pb[0] = xa; pb[1] = dw[2]; pb[2] = xb; pb[3] = dw[3]; }
+        else   { pb[0] = dw[0]; pb[1] = xa; pb[2] = dw[1]; pb[3] = xb; }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const v4i va = *reinterpret_cast<const v4i*>(Vt + vt_row(j * 32 + r32) + (2 * c + h) * 16);
+          acc2[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(va, pb, acc2[j], 0, 0, 0);
+        }
+      }
+      ctx_store(m, rp, acc2);
+    }
   }
 }
 
@@ -815,10 +1043,11 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
                     !getenv("NQK_ATTN_EXACT");
   const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + 256 + (size_t)(NT * 32 + 64) * 4;
   const dim3 grid((unsigned)batch_heads);
+  const size_t shm_tail = shm + attn_tail_lds<7, 197, true>();
   switch (T == 197 ? (fast ? -1 : 0) : NT) {
 #define A(n) case n: hipLaunchKernelGGL((k_attention<n, 0, false>), grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;
     case -1:  // ViT at 224 px (196 patches + CLS): the pairwise plan and pads fold at compile time
-      hipLaunchKernelGGL((k_attention<7, 197, true>), grid, dim3(256), shm, stream(), q, k, v, ctx, a);
+      hipLaunchKernelGGL((k_attention<7, 197, true>), grid, dim3(256), shm_tail, stream(), q, k, v, ctx, a);
       break;
     case 0:
       hipLaunchKernelGGL((k_attention<7, 197, false>), grid, dim3(256), shm, stream(), q, k, v, ctx, a);

@@ -284,4 +284,31 @@ r5_o() {
   echo done >> $STATUS
 }
 
+r5_p() {
+  # attention: the last row tile's 5 real rows by the row-parallel path (NQK_ATTN_TAIL, default on)
+  # against the 32-row form (tools/diag/libnqk_notail.so): parity, the kernel on the bench's data
+  # (both builds in one process), whole-bench A/B for both configs
+  rm -f $STATUS
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_b256.py tests/test_gpu_plan.py -x -q \
+    --timeout 300 --timeout-method thread > gpurun_out/p_tests.log 2>&1
+  step tests $?
+  AM_LIBS=notail=tools/diag/libnqk_notail.so timeout -k 10 300 python -u tools/attn_real.py > gpurun_out/p_attn_real.txt 2>&1
+  step attn_real $?
+  AB_LIBS="main notail" AB_REPS=3 OUT=p timeout -k 10 900 bash tools/ab.sh
+  step ab $?
+  LIB=numpy-quant_amd/numpy_quant/libnqk.so
+  cp $LIB /tmp/libnqk_main.so
+  for rep in 1 2; do
+    for v in main notail; do
+      if [ $v = main ]; then cp /tmp/libnqk_main.so $LIB; else cp tools/diag/libnqk_notail.so $LIB; fi
+      timeout -k 10 300 python -u bench.py --config vit_tiny --no-cpu-baseline --no-secondary --steps 20 \
+        > gpurun_out/p_tiny_${v}_$rep.json 2> gpurun_out/p_tiny_${v}_$rep.err
+      rc=$?
+      cp /tmp/libnqk_main.so $LIB
+      step tiny_${v}_$rep $rc
+    done
+  done
+  echo done >> $STATUS
+}
+
 "r5_$1"
