@@ -311,4 +311,20 @@ r5_p() {
   echo done >> $STATUS
 }
 
+r5_q() {
+  # the whole forward replayed as one captured hipGraph (bench.py --graph 1: no per-kernel host
+  # launches, the two parts' fork / join captured as graph edges) against eager issue, both configs
+  rm -f $STATUS
+  for rep in 1 2; do
+    for cfg in vit vit_tiny; do
+      for g in 0 1; do
+        timeout -k 10 300 python -u bench.py --config $cfg --graph $g --no-cpu-baseline --no-secondary --steps 20 \
+          > gpurun_out/q_${cfg}_g${g}_$rep.json 2> gpurun_out/q_${cfg}_g${g}_$rep.err
+        step ${cfg}_g${g}_$rep $?
+      done
+    done
+  done
+  echo done >> $STATUS
+}
+
 "r5_$1"
