@@ -481,7 +481,10 @@ def main(argv=None):
     ap.add_argument("--cpu-baseline", choices=("full", "layer"), default="full",
                     help="full: the oracle's whole ViT forward on one image (measured); layer: one layer x12")
     ap.add_argument("--no-secondary", action="store_true", help="skip the int4 / ViT-tiny / MLP-4096 lines")
-    ap.add_argument("--graph", type=int, default=0, help="1: replay the ViT forward as one captured hipGraph")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1 (default): replay the ViT forward as one captured hipGraph (QModel.graph: the fused "
+                         "plan's launches of both batch parts, captured once); 0: issue them from Python every step "
+                         "(+0.5 .. 0.9 %% with the graph, profiles/r05_graph_ab.txt)")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)  # launcher test: no GPU
     args = ap.parse_args(argv)
 
@@ -532,7 +535,7 @@ def run_secondary(args, group) -> dict:
     for cfg in ("vit_int4", "vit_tiny", "mlp4096"):
         sub = copy.copy(args)
         sub.config, sub.steps, sub.warmup, sub.no_cpu_baseline = cfg, min(args.steps, 10), min(args.warmup, 2), True
-        sub.graph = 0
+        sub.graph = args.graph
         t0 = time.time()
         try:
             r = run_mlp(sub, group) if cfg == "mlp4096" else run_vit(sub, group)
