@@ -327,4 +327,13 @@ r5_q() {
   echo done >> $STATUS
 }
 
+r5_r() {
+  # 256 x 256 B-shared tiles (NQK_PG_WM=2) against the shipped 128 x 256 form in the default bench
+  # (hipGraph replay, two parts), 3 interleaved reps
+  rm -f $STATUS
+  AB_ENVS="wm2:NQK_PG_WM=2" AB_REPS=3 OUT=r timeout -k 10 900 bash tools/ab.sh
+  step ab $?
+  echo done >> $STATUS
+}
+
 "r5_$1"
