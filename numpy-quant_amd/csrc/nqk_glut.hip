@@ -148,10 +148,20 @@ extern "C" int nqk_gelu_lut_build(float s_out, int64_t zp_out, int32_t bit_width
   // the first that fits GLUT_MAX; a candidate whose exhaustive check fails gives way to the next
   // (round 5: ViT-Ti's FFN-up outputs, s ~ 0.0052 .. 0.0058, need ~650 entries at (0.75 s, 3 s),
   // ~520 at (0.85 s, 6 s), ~500 at (0.88 s, 7 s))
+  // Single-line candidates first (fl = 0, round 5): the steep line on both branches (finer than
+  // needed on the decreasing one, so more entries), u = med3(R(h), ...) — the epilogue saves the L
+  // fma and the max (k_pg<PG_GLUT1>); the table reports iwL = 0, cL = -inf (max(R, L) = R, so the
+  // two-line kernel reads it the same way).  Every candidate passes the same exhaustive check (a
+  // bucket whose output changes twice fails it and the next candidate is tried).  NQK_GLUT_NO1=1
+  // skips them.
   struct Cand { double fr, fl; };
-  const Cand cands[] = {{0.75, 3.0}, {0.85, 3.0}, {0.85, 6.0}, {0.88, 7.0}};
+  // (0.885 s, 7.7 s): just below the closest spacings 0.8858 s / 7.758 s (max |slope| 1.12890 / 0.12890):
+  // ViT-Ti's smallest scales (s ~ 0.0052) fit 512 entries with it (508 against 517 at (0.88, 7)),
+  // so every ViT-Ti layer stays on the 128 x 256 kernel (NQK_GLUT_NOWIDE=1 drops it)
+  const Cand cands[] = {{0.75, 0.0}, {0.85, 0.0}, {0.88, 0.0}, {0.75, 3.0}, {0.85, 3.0}, {0.85, 6.0}, {0.88, 7.0}, {0.885, 7.7}};
+  const bool no1 = getenv("NQK_GLUT_NO1") != nullptr, nowide = getenv("NQK_GLUT_NOWIDE") != nullptr;
   auto count = [&](const Cand& c, int& nl_) {
-    const double wr_ = c.fr * s, wl_ = c.fl * s;
+    const double wr_ = c.fr * s, wl_ = c.fl > 0.0 ? c.fl * s : wr_;
     nl_ = (int)std::ceil((hk - (hl - 2.0 * wl_)) / wl_);
     const int nr_ = (int)std::ceil(((hr + 2.0 * wr_) - hk) / wr_);
     return nl_ + nr_ + 2;
@@ -163,7 +173,7 @@ extern "C" int nqk_gelu_lut_build(float s_out, int64_t zp_out, int32_t bit_width
       const int n_ = count(c, nl_);
       bool seen = false;
       for (const Cand& o : order) seen = seen || (o.fr == c.fr && o.fl == c.fl);
-      if (n_ >= 3 && n_ <= cap && !seen) order.push_back(c);
+      if (n_ >= 3 && n_ <= cap && !seen && !(no1 && c.fl == 0.0) && !(nowide && c.fr == 0.885)) order.push_back(c);
     }
   if (order.empty()) return 0;
   GLutQ q;
@@ -186,13 +196,13 @@ extern "C" int nqk_gelu_lut_build(float s_out, int64_t zp_out, int32_t bit_width
   for (const Cand& c : order) {
     int nl = 0;
     const int n = count(c, nl);
-    const double wr = c.fr * s, wl = c.fl * s;
+    const double wr = c.fr * s, wl = c.fl > 0.0 ? c.fl * s : wr;
     const double M = GLUT_MAGIC;
     GLutK k;
     k.iwR = (float)(1.0 / wr);
     k.cR = (float)(M + nl + 1 - hk * (double)k.iwR);
-    k.iwL = (float)(1.0 / wl);
-    k.cL = (float)(M + nl + 1 - hk * (double)k.iwL);
+    k.iwL = c.fl > 0.0 ? (float)(1.0 / wl) : 0.0f;
+    k.cL = c.fl > 0.0 ? (float)(M + nl + 1 - hk * (double)k.iwL) : -INFINITY;
     k.uhi = (float)(M + n - 1);
     int rc = check(hipMemsetAsync(err, 0, 4, stream()), "nqk_gelu_lut_build(memset)");
     if (rc) return done(rc);

@@ -8,6 +8,7 @@ bool pg_dispatch_i4(int key, const PgArgs& x) {
     NQK_PG_CASE(PG_QKV, 12, true, true, false, 1)
     NQK_PG_CASE(PG_GELU, 12, true, true, false, 1)
     NQK_PG_CASE(PG_GLUT, 12, true, true, false, 1)
+    NQK_PG_CASE(PG_GLUT1, 12, true, true, false, 1)
     NQK_PG_CASE(PG_RESID, 12, true, true, false, 1)
     NQK_PG_CASE(PG_RESID, 12, false, true, false, 1)
     NQK_PG_CASE(PG_RESID, 48, true, true, false, 1)

@@ -9,6 +9,7 @@ bool pg_dispatch_i8(int key, const PgArgs& x) {
     NQK_PG_CASE(PG_QKV, 12, true, false, false, 1)
     NQK_PG_CASE(PG_GELU, 12, true, false, false, 1)
     NQK_PG_CASE(PG_GLUT, 12, true, false, false, 1)
+    NQK_PG_CASE(PG_GLUT1, 12, true, false, false, 1)
     default:
       return false;
   }

@@ -9,6 +9,7 @@ bool pg_dispatch_tiny(int key, const PgArgs& x) {
     NQK_PG_CASE(PG_QKV, 3, true, false, false, 1)
     NQK_PG_CASE(PG_GELU, 3, true, false, false, 1)
     NQK_PG_CASE(PG_GLUT, 3, true, false, false, 1)
+    NQK_PG_CASE(PG_GLUT1, 3, true, false, false, 1)
     NQK_PG_CASE(PG_RESID, 3, true, false, false, 1)
     NQK_PG_CASE(PG_RESID, 3, false, false, false, 1)
     // the weight panel resident (RB)
@@ -16,7 +17,9 @@ bool pg_dispatch_tiny(int key, const PgArgs& x) {
     NQK_PG_CASE_RB(PG_QKV, 3, true, false, false, 1, true)
     NQK_PG_CASE_RB(PG_GELU, 3, true, false, false, 1, true)
     NQK_PG_CASE_RB(PG_GLUT, 3, true, false, false, 1, true)
+    NQK_PG_CASE_RB(PG_GLUT1, 3, true, false, false, 1, true)
     NQK_PG_CASE_RB(PG_GLUT, 3, true, false, false, 2, true)
+    NQK_PG_CASE_RB(PG_GLUT1, 3, true, false, false, 2, true)
     default:
       return false;
   }

@@ -9,7 +9,9 @@ bool pg_dispatch_wm2(int key, const PgArgs& x) {
     NQK_PG_CASE(PG_QKV, 12, true, false, false, 2)
     NQK_PG_CASE(PG_GELU, 12, true, false, false, 2)
     NQK_PG_CASE(PG_GLUT, 12, true, false, false, 2)
+    NQK_PG_CASE(PG_GLUT1, 12, true, false, false, 2)
     NQK_PG_CASE(PG_GLUT, 3, true, false, false, 2)
+    NQK_PG_CASE(PG_GLUT1, 3, true, false, false, 2)
     NQK_PG_CASE(PG_RESID, 12, true, false, false, 2)
     NQK_PG_CASE(PG_RESID, 12, false, false, false, 2)
     NQK_PG_CASE(PG_RESID, 48, true, false, false, 2)

@@ -190,7 +190,8 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   const char* wgpc = getenv("NQK_PG_WGPC");
   const int slots = (wm == 2 || (wgpc && atoi(wgpc) == 1) ? 1 : 2) * pg_num_cus();
   const int kc = K == 3072 ? 2 : (K == 192 ? 1 : 0);
-  const int epi_k = glut ? PG_GLUT : epi;
+  // a single-line table (lut_k[2] == 0: the L line is -inf) takes the epilogue without it
+  const int epi_k = glut ? (p->lut_k[2] == 0.0f ? PG_GLUT1 : PG_GLUT) : epi;
   const bool s8 = epi == PG_QKV && p->bit_width == 8 && !b4 && !getenv("NQK_PG_NOS8");
   // K = 192 (three k steps): NQK_PG_RB=1 keeps the weight panel resident (RB; measured no faster
   // at the ViT-Ti shapes: QKV 23.4 vs 23.4 us, GELU table 34.6 vs 34.9, profiles/r05_tiny_rb_embed_ab.txt)

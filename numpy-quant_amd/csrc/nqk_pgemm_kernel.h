@@ -55,6 +55,8 @@ constexpr int PG_PW = 2 + 4;                      // LDS-DMA pieces per wave per
 
 enum { PG_QKV = 0, PG_RESID = 3, PG_GELU = 4 };  // = the EPI_* codes of nqk_fused.hip
 constexpr int PG_GLUT = 5;  // GELU by table lookup (nqk_glut.h): launched for PG_GELU when a table is given
+constexpr int PG_GLUT1 = 6;  // ... with a single-line bucket coordinate (round 5: one pk_fma + the max fewer)
+constexpr bool pg_is_glut(int epi) { return epi == PG_GLUT || epi == PG_GLUT1; }
 // k_pg's LDS: a 3-stage ring of A (128 x 64 B) + B (256 rows x 64 B, or 32 B of int4
 // nibbles) per stage, the column constants (2 x 2 KiB), then the GELU table (PG_GLUT, 4 KiB)
 // or, for int4 weights, the residual epilogue's transpose scratch (int8: ring slot 2)
@@ -71,7 +73,7 @@ constexpr int pg_rd(int epi, int wm, int nk) { return (wm == 2 && epi != PG_RESI
 constexpr int pg_stg(bool b4, int wm = 1) { return PG_ASTG * wm + PG_BN * (b4 ? PG_BK / 2 : PG_BK); }
 constexpr int pg_colp(bool b4, int wm = 1, int rd = PG_RD) { return rd * pg_stg(b4, wm); }
 constexpr int pg_lds_bytes(int epi, bool b4, int wm = 1, int nk = 12) {
-  return pg_colp(b4, wm, pg_rd(epi, wm, nk)) + 4096 + (epi == PG_GLUT ? 8 * (wm == 2 ? GLUT_MAX : GLUT_CAP1) : 0) +
+  return pg_colp(b4, wm, pg_rd(epi, wm, nk)) + 4096 + (pg_is_glut(epi) ? 8 * (wm == 2 ? GLUT_MAX : GLUT_CAP1) : 0) +
          ((b4 || wm == 2) && epi == PG_RESID ? 4 * wm * 16 * PG_TR_ROW : 0);
 }
 
@@ -594,7 +596,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         } else {
           off = (uint32_t)(m * e.ldo + col0);
         }
-        if constexpr (EPI == PG_GLUT) {
+        if constexpr (pg_is_glut(EPI)) {
           // GELU by table lookup: h exactly as the reference (F32X), its bucket entry from
           // the LDS table (one ds_read_b64 per element), the output byte selected by one
           // compare (nqk_glut.h); no filter and no fallback path
@@ -607,12 +609,13 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
             const v2f vf = v2f{(float)av4[q & 3], (float)av4[(q & 3) + 1]};
             const v2f h = v2f{bias[q], bias[q + 1]} + vf * v2f{sacc, sacc};
             const v2f r = __builtin_elementwise_fma(h, v2f{e.gk.iwR, e.gk.iwR}, v2f{e.gk.cR, e.gk.cR});
-            const v2f l = __builtin_elementwise_fma(h, v2f{e.gk.iwL, e.gk.iwL}, v2f{e.gk.cL, e.gk.cL});
+            // PG_GLUT1: one line over both branches (the table's L line is -inf: max(R, L) = R)
+            const v2f l = EPI == PG_GLUT1 ? r : __builtin_elementwise_fma(h, v2f{e.gk.iwL, e.gk.iwL}, v2f{e.gk.cL, e.gk.cL});
             hv[q] = h[0];
             hv[q + 1] = h[1];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-              const float u = __builtin_amdgcn_fmed3f(__builtin_fmaxf(r[j], l[j]), GLUT_MAGIC, e.gk.uhi);
+              const float u = __builtin_amdgcn_fmed3f(EPI == PG_GLUT1 ? r[j] : __builtin_fmaxf(r[j], l[j]), GLUT_MAGIC, e.gk.uhi);
               const uint32_t a = (__float_as_uint(u) << 3) + lut_base;
               const v2u t = *(const __attribute__((address_space(3))) v2u*)(uintptr_t)a;
               ent[q + j] = make_uint2(t[0], t[1]);
@@ -843,7 +846,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     // VMEM operations per wave, in issue order: [B pieces when the panel changes], colp(next),
     // the next tile's A pieces (3 k steps), then the epilogue's EOPS stores: waiting for all but
     // EOPS waits for everything the next tile reads
-    if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
+    if constexpr (pg_is_glut(EPI)) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
     auto issue_b = [&](const Src& s) __attribute__((always_inline)) {
 #pragma unroll
       for (int kt = 0; kt < NK; ++kt)
@@ -917,7 +920,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   }
   // PG_GLUT: the 4 KiB GELU table into LDS, 1 KiB per wave (waited for with stage 0)
   // (WM = 2: the 8 KiB of a table of up to GLUT_MAX entries, 1 KiB per wave as well)
-  if constexpr (EPI == PG_GLUT) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
+  if constexpr (pg_is_glut(EPI)) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
   issue_colp(cur.tn, 0);
   sfor<0, RD - 1>([&](auto S) __attribute__((always_inline)) { issue_stage(cur, decltype(S)::value, decltype(S)::value); });
   if constexpr (NQK_PG_PRIO == 2) {

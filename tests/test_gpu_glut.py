@@ -44,8 +44,17 @@ CASES = [(0.012436897, -114, 8), (0.010944091, -112, 8), (0.0165, -118, 8), (0.0
 
 
 @pytest.mark.parametrize("s_out,zp,bw", CASES)
-def test_gelu_table_is_exact_on_every_float(s_out, zp, bw):
+@pytest.mark.parametrize("no1", [False, True])
+def test_gelu_table_is_exact_on_every_float(s_out, zp, bw, no1, monkeypatch):
+    """no1: NQK_GLUT_NO1=1, two-line bucket coordinates only (round 5 tries a single line first:
+    k[2] == 0, the k_pg<PG_GLUT1> epilogue)."""
+    if no1:
+        monkeypatch.setenv("NQK_GLUT_NO1", "1")
+    else:
+        monkeypatch.delenv("NQK_GLUT_NO1", raising=False)
     lut, k, n = _build(s_out, zp, bw)
+    if no1:
+        assert k[2] != 0.0
     # small scales need more than the 128 x 256-tile kernel's 512 buckets: up to 1024 (the
     # 256 x 256-tile kernel's LDS)
     assert 0 < n <= (1024 if s_out < 0.006 else 512), n
@@ -131,9 +140,15 @@ def _gelu_gemm(M, N, K, s_out, zp, seed, table, monkeypatch, wm=0, wbits=8):
     (256 * 197, 768, 192, 0.00521903, -95), (128 * 50 + 77, 3072, 768, 0.0027, -9),
 ])
 @pytest.mark.parametrize("wm", [1, 2])
-def test_pg_gelu_table_equals_filtered_chain(M, N, K, s_out, zp, wm, monkeypatch):
+@pytest.mark.parametrize("no1", [False, True])
+def test_pg_gelu_table_equals_filtered_chain(M, N, K, s_out, zp, wm, no1, monkeypatch):
     """wm 2: the 256 x 256-tile form of k_pg (both sides; K = 192 and M < 256 stay 128-row),
-    and a table of more than 512 entries takes that form whatever wm says."""
+    and a table of more than 512 entries takes that form whatever wm says.  no1: two-line tables
+    only (else a single-line table, k_pg<PG_GLUT1>, where one fits first)."""
+    if no1:
+        monkeypatch.setenv("NQK_GLUT_NO1", "1")
+    else:
+        monkeypatch.delenv("NQK_GLUT_NO1", raising=False)
     k0, ref = _gelu_gemm(M, N, K, s_out, zp, M + N, False, monkeypatch, wm)
     k1, got = _gelu_gemm(M, N, K, s_out, zp, M + N, True, monkeypatch, wm)
     two = wm == 2 and K != 192 and M >= 256

@@ -336,4 +336,24 @@ r5_r() {
   echo done >> $STATUS
 }
 
+r5_s() {
+  # GELU tables: single-line bucket coordinates (k_pg<PG_GLUT1>, where they fit first) and the
+  # (0.885 s, 7.7 s) two-line candidate that keeps ViT-Ti's tables within 512 entries: parity (both
+  # table kinds), then ViT-Ti whole bench against the previous candidate set (NQK_GLUT_NO1=1
+  # NQK_GLUT_NOWIDE=1), 3 interleaved reps
+  rm -f $STATUS
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_glut.py tests/test_gpu_b256.py -x -q --timeout 300 \
+    --timeout-method thread > gpurun_out/s_tests.log 2>&1
+  step tests $?
+  for rep in 1 2 3; do
+    for v in main old; do
+      e=""; [ $v = old ] && e="NQK_GLUT_NO1=1 NQK_GLUT_NOWIDE=1"
+      env $e timeout -k 10 300 python -u bench.py --config vit_tiny --no-cpu-baseline --no-secondary --steps 20 \
+        > gpurun_out/s_tiny_${v}_$rep.json 2> gpurun_out/s_tiny_${v}_$rep.err
+      step tiny_${v}_$rep $?
+    done
+  done
+  echo done >> $STATUS
+}
+
 "r5_$1"
