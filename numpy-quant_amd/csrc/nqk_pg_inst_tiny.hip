@@ -10,6 +10,12 @@ bool pg_dispatch_tiny(int key, const PgArgs& x) {
     NQK_PG_CASE(PG_GELU, 3, true, false, false, 1)
     NQK_PG_CASE(PG_GLUT, 3, true, false, false, 1)
     NQK_PG_CASE(PG_GLUT1, 3, true, false, false, 1)
+    // 64-row tiles (WM = 0)
+    NQK_PG_CASE(PG_QKV, 3, true, false, true, 0)
+    NQK_PG_CASE(PG_QKV, 3, true, false, false, 0)
+    NQK_PG_CASE(PG_GELU, 3, true, false, false, 0)
+    NQK_PG_CASE(PG_GLUT, 3, true, false, false, 0)
+    NQK_PG_CASE(PG_GLUT1, 3, true, false, false, 0)
     NQK_PG_CASE(PG_RESID, 3, true, false, false, 1)
     NQK_PG_CASE(PG_RESID, 3, false, false, false, 1)
     // the weight panel resident (RB)

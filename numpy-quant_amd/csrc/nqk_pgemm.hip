@@ -183,7 +183,19 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
     const float g_abs = (float)(GELU_ABS * ars) + 0x1p-100f;
     e.g_lim = (float)((0.5 - (double)g_abs) * (1.0 - 0x1p-22));
   }
-  const int tiles_n = (int)((N + PG_BN - 1) / PG_BN), tiles_m = (int)((M + wm * PG_BM - 1) / (wm * PG_BM));
+  // K = 192 (three k steps): NQK_PG_RB=1 keeps the weight panel resident (RB; measured no faster
+  // at the ViT-Ti shapes: QKV 23.4 vs 23.4 us, GELU table 34.6 vs 34.9, profiles/r05_tiny_rb_embed_ab.txt)
+  const char* rbv = getenv("NQK_PG_RB");
+  const bool rb = K == 192 && !b4 && epi != PG_RESID && rbv && atoi(rbv) != 0;
+  // K = 192, QKV / GELU, int8: 64-row tiles with NQK_PG_WM0=1 (WM = 0; measured slower: the 128-row
+  // form's time is linear in its tiles, a partial last pass costs nothing extra, and the 64-row
+  // tiles read B twice per output — QKV 22.8 vs 19.2 us, profiles/r05_pg_rows64_dropped.txt)
+  {
+    const char* w0 = getenv("NQK_PG_WM0");
+    if (K == 192 && wm == 1 && epi != PG_RESID && !b4 && !rb && w0 && atoi(w0) == 1) wm = 0;
+  }
+  const int bm = wm ? wm * PG_BM : PG_BM / 2;
+  const int tiles_n = (int)((N + PG_BN - 1) / PG_BN), tiles_m = (int)((M + bm - 1) / bm);
   const int nt = tiles_m * tiles_n;
   // NQK_PG_WGPC=1: one workgroup per CU (the other half of the register file free for the other
   // stream's kernels: A/B switch with NQK_STREAM_LAG)
@@ -193,11 +205,8 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   // a single-line table (lut_k[2] == 0: the L line is -inf) takes the epilogue without it
   const int epi_k = glut ? (p->lut_k[2] == 0.0f ? PG_GLUT1 : PG_GLUT) : epi;
   const bool s8 = epi == PG_QKV && p->bit_width == 8 && !b4 && !getenv("NQK_PG_NOS8");
-  // K = 192 (three k steps): NQK_PG_RB=1 keeps the weight panel resident (RB; measured no faster
-  // at the ViT-Ti shapes: QKV 23.4 vs 23.4 us, GELU table 34.6 vs 34.9, profiles/r05_tiny_rb_embed_ab.txt)
-  const char* rbv = getenv("NQK_PG_RB");
-  const bool rb = K == 192 && !b4 && epi != PG_RESID && rbv && atoi(rbv) != 0;
-  const int key = epi_k * 16 + kc * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0) + (s8 ? 256 : 0) + (wm == 2 ? 512 : 0) + (rb ? 1024 : 0);
+  const int key = pg_key(epi_k, K == 3072 ? 48 : (K == 192 ? 3 : 12), f32x, b4, s8, wm, rb);
+  (void)kc;
   const PgArgs x{a, bp, (int)M, (int)N, (int)lda, tiles_n, nt, nt < slots ? nt : slots, &e};
   // (A tail split — the rows of the whole rounds in one launch, the last round's row panels
   // in a second launch with one workgroup per tile — measured slower: FFN-down 142 -> 176 us,

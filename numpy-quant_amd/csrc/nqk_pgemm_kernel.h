@@ -70,7 +70,7 @@ constexpr int PG_TR_ROW = 272;  // bytes per staged residual row (256 + 16: conf
 #endif
 // ring depth: 3 stages, or NQK_PG_WM2_RD for the 256 x 256 form where K is a multiple of 4 k steps
 constexpr int pg_rd(int epi, int wm, int nk) { return (wm == 2 && epi != PG_RESID && nk % 4 == 0) ? NQK_PG_WM2_RD : PG_RD; }
-constexpr int pg_stg(bool b4, int wm = 1) { return PG_ASTG * wm + PG_BN * (b4 ? PG_BK / 2 : PG_BK); }
+constexpr int pg_stg(bool b4, int wm = 1) { return (wm ? PG_ASTG * wm : PG_ASTG / 2) + PG_BN * (b4 ? PG_BK / 2 : PG_BK); }
 constexpr int pg_colp(bool b4, int wm = 1, int rd = PG_RD) { return rd * pg_stg(b4, wm); }
 constexpr int pg_lds_bytes(int epi, bool b4, int wm = 1, int nk = 12) {
   return pg_colp(b4, wm, pg_rd(epi, wm, nk)) + 4096 + (pg_is_glut(epi) ? 8 * (wm == 2 ? GLUT_MAX : GLUT_CAP1) : 0) +
@@ -379,25 +379,34 @@ constexpr float PG_QLIM = 0x1.fffffcp-2f;
 // when its next tile is in another panel, and streams only A (24 KiB -> 8 KiB of operand bytes
 // per tile: one third); the k loop runs without loads or barriers, the next tile's A is issued
 // right after it, under the epilogue.
+// WM = 0 (round 5, K = 192: ViT-Ti's QKV and FFN-up; opt-in NQK_PG_WM0=1): 64-row tiles — twice
+// the tiles, for a less partial last pass of the persistent grid (ViT-Ti B = 256: 2 364 tiles = 4.6
+// passes instead of 1 182 = 2.3); one A piece per wave per stage, the k step's 16 MFMAs (subtiles
+// 0..3) split 8 + 8 around the stage wait.  Measured slower (the 128-row form's time is linear in its
+// tiles; 64-row tiles read B twice per output), profiles/r05_pg_rows64_dropped.txt.
 template <int EPI, int NK, bool F32X, bool B4, bool S8 = false, int WM = 1, bool RB = false>
-__global__ void __launch_bounds__(256 * WM, 2 / WM)
+__global__ void __launch_bounds__(256 * (WM == 2 ? 2 : 1), WM == 2 ? 1 : 2)
 k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, int lda, int tiles_n, int ntiles,
      PgEpi e) {
   constexpr int RD = RB ? PG_RD : pg_rd(EPI, WM, NK);  // ring stages
   static_assert(NK % RD == 0 && (NK >= 2 * RD || NK == RD), "k_pg: NK a multiple of the ring depth");
   static_assert(RD == PG_RD || EPI != PG_RESID, "k_pg: the residual epilogue borrows ring slot 2 (3 stages)");
-  static_assert(WM == 1 || WM == 2, "k_pg: one or two 128-row halves per tile");
+  static_assert(WM == 0 || WM == 1 || WM == 2, "k_pg: a 64-row tile, or one or two 128-row halves per tile");
+  static_assert(WM != 0 || (!B4 && !RB && EPI != PG_RESID), "k_pg<WM = 0>: int8, QKV / GELU only");
+  constexpr int WQ = WM == 2 ? 2 : 1;            // 4-wave groups per workgroup
+  constexpr int APW = WM == 0 ? 1 : 2;           // A LDS-DMA pieces per wave per stage
+  constexpr int MS = WM == 0 ? 4 : 8;            // 16-row subtiles of a wave
   static_assert(!RB || (NK == PG_RD && !B4 && EPI != PG_RESID), "k_pg<RB>: K = 3 k steps, int8, not residual");
   constexpr bool RESID = EPI == PG_RESID;
-  constexpr int BM = PG_BM * WM;                // tile rows
-  constexpr int ASTG = PG_ASTG * WM;            // A bytes of a stage
+  constexpr int BM = WM ? PG_BM * WM : 64;      // tile rows
+  constexpr int ASTG = WM ? PG_ASTG * WM : PG_ASTG / 2;  // A bytes of a stage
   constexpr int BROW = B4 ? PG_BK / 2 : PG_BK;  // bytes of one B row per k-step
-  constexpr int NBP = (B4 ? 2 : 4) / WM;        // B LDS-DMA pieces per wave per stage
+  constexpr int NBP = (B4 ? 2 : 4) / WQ;        // B LDS-DMA pieces per wave per stage
   constexpr int STG = pg_stg(B4, WM), COLP = pg_colp(B4, WM, RD), LUTO = COLP + 4096;
-  constexpr int PW = 2 + NBP;                   // LDS-DMA pieces per wave per stage
+  constexpr int PW = APW + NBP;                 // LDS-DMA pieces per wave per stage
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & (4 * WM - 1));
+  const int wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & (4 * WQ - 1));
   const int wn = wave & 3, wm = WM == 2 ? wave >> 2 : 0;  // column quarter / row half of the tile
   const int l15 = lane & 15, lg = lane >> 4;
 
@@ -416,7 +425,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   const rsrc_t r_a = pg_rsrc(A, (uint32_t)((uint64_t)M * lda));
   const rsrc_t r_b = pg_rsrc(Bp, (uint32_t)((uint64_t)tiles_n * BSTRIDE));
   // LDS-DMA sources: A piece pp of wave w = rows 32 w + 16 pp + (l >> 2), physical chunk l & 3
-  const uint32_t va = (uint32_t)((32 * wave + (lane >> 2)) * lda + 16 * ((lane & 3) ^ pg_sw(lane >> 2)));
+  const uint32_t va = (uint32_t)((16 * APW * wave + (lane >> 2)) * lda + 16 * ((lane & 3) ^ pg_sw(lane >> 2)));
   const uint32_t vb = (uint32_t)(NBP * 1024 * wave + 16 * lane);
   // fragment offsets: row (l & 15) of a 16-row subtile, logical chunk l >> 4 (B4: 8-byte
   // chunks of 32-byte rows, chunk ^ 2 in rows 8..15 of a subtile: conflict-free b64 reads)
@@ -446,19 +455,19 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   auto issue_piece = [&](const Src& s, int kt, int slot, int p) __attribute__((always_inline)) {
     if constexpr ((NQK_PG_DIAG & 4) != 0) return;
     int8_t* st = lds + slot * STG;
-    if (p < 2) {
+    if (p < APW) {
       if constexpr ((NQK_PG_DIAG & 512) != 0) {
         // (diagnostic 512, wrong values: the A piece as 8 rows x 128 B — whole cache lines, rows
         // 8 (kt & 1) .. + 7 of the piece's 16 at the k-pair's 128-B block — the same bytes per step in
         // half the L1 -> L2 requests)
         const uint32_t v512 = (uint32_t)((32 * wave + 16 * p + 8 * (kt & 1) + (lane >> 3)) * lda + (lane & 7) * 16);
-        pg_dma16(r_a, st + (2 * wave + p) * 1024, v512, s.sa + (uint32_t)(kt & ~1) * PG_BK);
+        pg_dma16(r_a, st + (APW * wave + p) * 1024, v512, s.sa + (uint32_t)(kt & ~1) * PG_BK);
       } else if constexpr ((NQK_PG_DIAG & 256) == 0)  // (diagnostic 256: no A pieces, 128: no B pieces)
-        pg_dma16(r_a, st + (2 * wave + p) * 1024, va, s.sa + (uint32_t)p * 16u * (uint32_t)lda + kt * PG_BK);
+        pg_dma16(r_a, st + (APW * wave + p) * 1024, va, s.sa + (uint32_t)p * 16u * (uint32_t)lda + kt * PG_BK);
     } else {
       if constexpr ((NQK_PG_DIAG & 128) == 0)
-        pg_dma16(r_b, st + ASTG + (NBP * wave + p - 2) * 1024, vb,
-                 s.sb + (uint32_t)(kt * (PG_BN * BROW) + (p - 2) * 1024));
+        pg_dma16(r_b, st + ASTG + (NBP * wave + p - APW) * 1024, vb,
+                 s.sb + (uint32_t)(kt * (PG_BN * BROW) + (p - APW) * 1024));
     }
   };
   auto issue_stage = [&](const Src& s, int kt, int slot) __attribute__((always_inline)) {
@@ -471,11 +480,11 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   const rsrc_t r_ct = pg_rsrc(e.colterm, (uint32_t)((uint64_t)N * 4));
   const rsrc_t r_bias = pg_rsrc(e.bias, e.bias ? (uint32_t)((uint64_t)N * 4) : 0u);
   auto issue_colp = [&](int tn, int cslot) __attribute__((always_inline)) {
-    constexpr int CB = 512 / WM, CL = 32 / WM;  // bytes / lanes per wave
+    constexpr int CB = 512 / WQ, CL = 32 / WQ;  // bytes / lanes per wave
     int8_t* dst = lds + COLP + cslot * 2048 + wave * CB;
-    const uint32_t voff = (uint32_t)((tn * PG_BN + (wave % (2 * WM)) * (CB / 4) + (lane & (CL - 1)) * 4) * 4);
+    const uint32_t voff = (uint32_t)((tn * PG_BN + (wave % (2 * WQ)) * (CB / 4) + (lane & (CL - 1)) * 4) * 4);
     if (lane < CL) {
-      if (wave < 2 * WM) pg_dma16(r_ct, dst, voff, 0);
+      if (wave < 2 * WQ) pg_dma16(r_ct, dst, voff, 0);
       else pg_dma16(r_bias, dst, voff, 0);  // bias == null: the descriptor returns zeros
     }
   };
@@ -519,6 +528,22 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         acc[4 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], ci[j], 0, 0, 0);
       else
         acc[4 * h + ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], acc[4 * h + ii][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      fn(Q);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+
+  // 8 MFMAs (subtiles 2 qi, 2 qi + 1) with fn(q) after MFMA q: the 64-row form (WM = 0)
+  auto quarter = [&](auto QI, auto FIRST, const v4i (&aa)[4], const v4i (&bb)[4], const v4i (&ci)[4], auto&& fn)
+      __attribute__((always_inline)) {
+    constexpr int qi = decltype(QI)::value;
+    sfor<0, 8>([&](auto Q) __attribute__((always_inline)) {
+      constexpr int q = decltype(Q)::value, ii = 2 * qi + (q >> 2), j = q & 3;
+      if constexpr (decltype(FIRST)::value)
+        acc[ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], ci[j], 0, 0, 0);
+      else
+        acc[ii][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bb[j], aa[ii], acc[ii][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       fn(Q);
       __builtin_amdgcn_sched_barrier(0);
@@ -586,7 +611,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       }
       int hh = 0;
       if constexpr (EPI == PG_QKV) hh = (cw - g3 * e.group_cols) / e.hdim;
-      sfor<0, 8>([&](auto I) __attribute__((always_inline)) {
+      sfor<0, MS>([&](auto I) __attribute__((always_inline)) {
         constexpr int i = decltype(I)::value;
         const int m = s.r0 + PG_BM * wm + 16 * i + l15;
         uint32_t off;
@@ -839,7 +864,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   // stages 0 and 1, then the epilogue's operations (EOPS)
   // RESID: 8 x 4 stores after the stages (counted conservatively without the 6 x 4 residual
   // loads, which the compiler may hoist above the stage issues: a smaller count only waits more)
-  constexpr int EOPS = RESID ? 32 : 8;
+  constexpr int EOPS = RESID ? 32 : MS;
   constexpr int PWA = PW;
   Src cur = src_of(tile_at(0));
   if constexpr (RB) {
@@ -964,6 +989,34 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       v4i(&bn)[4] = (kt & 1) ? b0 : b1;
       v2u(&pc)[4] = (kt & 1) ? p1 : p0;
       v2u(&pn)[4] = (kt & 1) ? p0 : p1;
+      if constexpr (WM == 0) {
+        // 64-row form: this step's A fragments (subtiles 0..3) alternate between a_lo and a_hi;
+        // MFMAs of subtiles 0, 1 (the refill of the slot step kt - 1 read after MFMA 4), the wait
+        // for stage kt + 1, then subtiles 2, 3 with the next step's fragment reads between them
+        v4i(&ac)[4] = (kt & 1) ? a_hi : a_lo;
+        v4i(&an)[4] = (kt & 1) ? a_lo : a_hi;
+        if constexpr (kt > 0) pg_lgkm_tie8(ac, bc);
+        quarter(ic<0>{}, std::integral_constant<bool, kt == 0>{}, ac, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
+          if constexpr (kt + RD - 1 < NK && decltype(Q)::value == 4) issue_stage(cur, kt + RD - 1, (kt + RD - 1) % RD);
+        });
+        if constexpr (kt == 1) issue_colp(nxt.tn, cs ^ 1);
+        if constexpr (kt + 1 < NK) {
+          constexpr int hi_s = (kt + RD - 1 < NK ? kt + RD - 1 : NK - 1);
+          constexpr int y = (hi_s >= kt + 2 ? (hi_s - kt - 1) * PWA : 0) + ((kt >= 1 && kt <= RD - 1) ? 1 : 0);
+          if (kt + 1 <= RD - 2 && it > 0) pg_vmcnt<y + EOPS>();
+          else pg_vmcnt<y>();
+          if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        quarter(ic<1>{}, std::integral_constant<bool, kt == 0>{}, ac, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
+          constexpr int q = decltype(Q)::value;
+          if constexpr (kt + 1 < NK) {
+            if constexpr (q < 4) rd_a(an, ic<(kt + 1) % RD>{}, ic<0>{}, Q);
+            else rd_b(bn, ic<(kt + 1) % RD>{}, ic<q - 4>{});
+          }
+        });
+        return;
+      }
       if constexpr (kt > 0) {  // this step's fragments (read in step kt - 1)
         if constexpr (B4) {
           pg_lgkm_tie_a4(a_lo, pc);
@@ -1059,14 +1112,14 @@ bool pg_dispatch_tiny(int key, const PgArgs& x);
 bool pg_dispatch_i4(int key, const PgArgs& x);
 bool pg_dispatch_wm2(int key, const PgArgs& x);
 
-// launch keys: EPI * 16 + (K 3072: 2, K 192: 1, else 0) * 4 + F32X + 2 B4 + 256 S8 + 512 WM2 + 1024 RB
+// launch keys: EPI * 16 + (K 3072: 2, K 192: 1, else 0) * 4 + F32X + 2 B4 + 256 S8 + 512 WM2 + 1024 RB + 2048 WM0
 constexpr int pg_key(int epi, int nk, bool f32x, bool b4, bool s8, int wm, bool rb = false) {
   return epi * 16 + (nk == 48 ? 2 : (nk == 3 ? 1 : 0)) * 4 + (f32x ? 1 : 0) + (b4 ? 2 : 0) + (s8 ? 256 : 0) +
-         (wm == 2 ? 512 : 0) + (rb ? 1024 : 0);
+         (wm == 2 ? 512 : 0) + (rb ? 1024 : 0) + (wm == 0 ? 2048 : 0);
 }
 #define NQK_PG_CASE_RB(E, NKV, X, B, S, W, R)                                                                  \
   case pg_key(E, NKV, X, B, S, W, R):                                                                          \
-    hipLaunchKernelGGL((k_pg<E, NKV, X, B, S, W, R>), dim3(x.grid), dim3(256 * W), pg_lds_bytes(E, B, W, NKV), stream(), \
+    hipLaunchKernelGGL((k_pg<E, NKV, X, B, S, W, R>), dim3(x.grid), dim3(W == 2 ? 512 : 256), pg_lds_bytes(E, B, W, NKV), stream(), \
                        x.a, x.bp, x.m, x.n, x.lda, x.tiles_n, x.ntiles, *static_cast<const PgEpi*>(x.epi));    \
     return true;
 #define NQK_PG_CASE(E, NKV, X, B, S, W) NQK_PG_CASE_RB(E, NKV, X, B, S, W, false)

@@ -137,12 +137,17 @@ def test_pg_gemm_equals_big_tile(epi_name, M, N, K, s_out_scale, no_f32x, kernel
 @pytest.mark.parametrize("epi_name,M,N,K,s_out_scale,no_f32x", [
     ("qkv", 256 * 197, 576, 192, 1.0, False), ("qkv", 197 * 3, 576, 192, 0.05, False),
     ("gelu", 128 * 197, 768, 192, 1.0, False), ("gelu", 300, 768, 192, 0.1, False),
+    # ragged last 64-row tiles, more tiles than workgroup slots
+    ("qkv", 197 * 13, 576, 192, 1.0, False), ("gelu", 64 * 1100 + 5, 768, 192, 1.0, False),
 ])
-def test_pg_gemm_vit_tiny_shapes(epi_name, M, N, K, s_out_scale, no_f32x, monkeypatch):
+@pytest.mark.parametrize("rows", [64, 128])
+def test_pg_gemm_vit_tiny_shapes(epi_name, M, N, K, s_out_scale, no_f32x, rows, monkeypatch):
     """ViT-Ti/16 widths (D = 192, 3 heads, MLP 768): K = 192 (a 3-step k loop) and N % 256 != 0
     (QKV 576: the last column tile's waves past N store through zero-size descriptors) — k_pg
     equals the one-tile-per-workgroup kernel bit for bit, and the NumPy chain for the small
-    QKV case.  (Residual epilogues at N = 192 stay on the other kernel: faster there.)"""
+    QKV case.  rows: the 64-row tile form (WM = 0, round 5, opt-in NQK_PG_WM0=1) and the
+    128-row one.  (Residual epilogues at N = 192 stay on the other kernel.)"""
+    monkeypatch.setenv("NQK_PG_WM0", "1" if rows == 64 else "0")
     seed = M + N + K + 1
     k0, ref, host = _run(epi_name, M, N, K, s_out_scale, False, no_f32x, monkeypatch, seed, 1)
     k1, got, _ = _run(epi_name, M, N, K, s_out_scale, True, no_f32x, monkeypatch, seed, 1)

@@ -27,7 +27,8 @@ main = _lib.load()
 M = int(os.environ.get("GM_M", 256 * 197))
 REPS = int(os.environ.get("PGM_REPS", 20))
 ROUNDS = int(os.environ.get("PGM_ROUNDS", 3))
-shapes = {"qkv": (2304, 768, 0), "out": (768, 768, 3), "up": (3072, 768, 4), "down": (768, 3072, 3)}
+shapes = {"qkv": (2304, 768, 0), "out": (768, 768, 3), "up": (3072, 768, 4), "down": (768, 3072, 3),
+          "tqkv": (576, 192, 0), "tup": (768, 192, 4)}  # (t*: ViT-Ti, K = 192)
 sel = os.environ.get("PGM_SHAPES", "qkv,out,up,down").split(",")
 rng = np.random.default_rng(0)
 
@@ -63,11 +64,13 @@ def setup(name):
     bias = DeviceArray.from_host((0.01 * rng.standard_normal(N)).astype(np.float32))
     resid = DeviceArray.from_host(rng.standard_normal((M, N)).astype(np.float32))
     out = DeviceArray((M, N), np.float32)
-    outs = [DeviceArray((M, 768), np.int8) for _ in range(3)] if epi == 0 else [out]
+    D = N // 3 if epi == 0 else 768  # the model width (QKV: N = 3 D)
+    # QKV writes the head layout of whole images: ceil(M / 197) of them
+    outs = [DeviceArray((-(-M // 197) * 197, D), np.int8) for _ in range(3)] if epi == 0 else [out]
     e = _lib.Epilogue()
     e.zp_flags, e.bit_width = _lib.ZP_COL, 8
-    e.group_cols = 768 if epi == 0 else (1 << 30)
-    e.tokens, e.heads, e.hdim = 197, 12, 64
+    e.group_cols = D if epi == 0 else (1 << 30)
+    e.tokens, e.heads, e.hdim = 197, D // 64, 64
     e.zpa, e.col, e.colterm, e.col_absmax = 3, col.ptr, colterm.ptr, 1
     for g in range(3):
         e.s_acc[g] = 7e-6 * (768 / K) ** 0.5

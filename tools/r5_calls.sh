@@ -356,4 +356,39 @@ r5_s() {
   echo done >> $STATUS
 }
 
+r5_t() {
+  # ViT-Ti's K = 192 GEMMs (QKV, FFN-up + GELU table) at M giving exactly 2 / 2.31 / 3 passes of
+  # 128 x 256 tiles over the 512 workgroup slots: how much does the partial last pass cost?
+  rm -f $STATUS
+  for m in 43648 50432 65536; do
+    GM_M=$m PGM_SHAPES=tqkv,tup PGM_ROUNDS=3 timeout -k 10 300 python -u tools/pg_micro.py > gpurun_out/t_pg_micro_$m.txt 2>&1
+    step micro_$m $?
+  done
+  echo done >> $STATUS
+}
+
+r5_u() {
+  # k_pg 64-row tiles at K = 192 (WM = 0, default) against 128-row (NQK_PG_WM0=0): parity (ViT-Ti
+  # shapes, GELU tables, the ViT-Ti forward in the plan tests), the kernel micro at M giving 2 /
+  # 2.31 / 3 passes of 128-row tiles, then ViT-Ti whole bench, 3 interleaved reps
+  rm -f $STATUS
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_pgemm.py tests/test_gpu_glut.py tests/test_gpu_plan.py -x -q \
+    --timeout 300 --timeout-method thread > gpurun_out/u_tests.log 2>&1
+  step tests $?
+  for m in 43648 50432 65536; do
+    GM_M=$m PGM_SHAPES=tqkv,tup PGM_ROUNDS=3 PGM_ENV="r128:NQK_PG_WM0=0" timeout -k 10 300 python -u tools/pg_micro.py \
+      > gpurun_out/u_pg_micro_$m.txt 2>&1
+    step micro_$m $?
+  done
+  for rep in 1 2 3; do
+    for v in main r128; do
+      e=""; [ $v = r128 ] && e="NQK_PG_WM0=0"
+      env $e timeout -k 10 300 python -u bench.py --config vit_tiny --no-cpu-baseline --no-secondary --steps 20 \
+        > gpurun_out/u_tiny_${v}_$rep.json 2> gpurun_out/u_tiny_${v}_$rep.err
+      step tiny_${v}_$rep $?
+    done
+  done
+  echo done >> $STATUS
+}
+
 "r5_$1"
