@@ -391,4 +391,16 @@ r5_u() {
   echo done >> $STATUS
 }
 
+r5_v() {
+  # the round's final tree: every GPU test, smoke(), a default bench line
+  rm -f $STATUS
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/v_tests.log 2>&1
+  step tests $?
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/v_smoke.log 2>&1
+  step smoke $?
+  timeout -k 10 400 python -u bench.py > gpurun_out/v_bench.json 2> gpurun_out/v_bench.err
+  step bench $?
+  echo done >> $STATUS
+}
+
 "r5_$1"
