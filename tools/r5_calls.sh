@@ -403,4 +403,13 @@ r5_v() {
   echo done >> $STATUS
 }
 
+r5_w() {
+  # with the hipGraph replay default: one stream part (NQK_SPLIT=0) and the persistent LayerNorm
+  # (NQK_LN_PERS=4) against the shipped two parts / one-shot LN, whole bench, 3 interleaved reps
+  rm -f $STATUS
+  AB_ENVS="split0:NQK_SPLIT=0 lnp4:NQK_LN_PERS=4" AB_REPS=3 OUT=w timeout -k 10 1100 bash tools/ab.sh
+  step ab $?
+  echo done >> $STATUS
+}
+
 "r5_$1"
