@@ -215,8 +215,9 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int tok = 4 * rb + r;
-      w[r] = (tok < T && (NQK_ATTN_DIAG & 64) == 0) ? *reinterpret_cast<const v4i*>(v + tok * 64 + c * 16)
-                                                      : v4i{0, 0, 0, 0};
+      // (diagnostic 64: no K / V loads; 4096: no V loads)
+      w[r] = (tok < T && (NQK_ATTN_DIAG & (64 | 4096)) == 0) ? *reinterpret_cast<const v4i*>(v + tok * 64 + c * 16)
+                                                               : v4i{0, 0, 0, 0};
     }
 #if NQK_ATTN_DIAG & 1  // diagnostic builds only (wrong results): 1 = V^T staging skipped, 2 = exp
                       // replaced by one add, 4 = P quantize replaced by a convert

@@ -412,4 +412,14 @@ r5_w() {
   echo done >> $STATUS
 }
 
+r5_x() {
+  # attention: what the V staging alone costs (diagnostic 4096: V loads skipped, K kept; 64: both
+  # skipped), the bench's data, one process
+  rm -f $STATUS
+  AM_LIBS=a4096=tools/diag/libnqk_a4096.so,a64=tools/diag/libnqk_a64.so timeout -k 10 300 python -u tools/attn_real.py \
+    > gpurun_out/x_attn_real.txt 2>&1
+  step attn_real $?
+  echo done >> $STATUS
+}
+
 "r5_$1"
