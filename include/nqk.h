@@ -289,7 +289,8 @@ int nqk_pack_pg4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t l
 /* The FFN-up epilogue's GELU chain as a table (round 4; up to 1024 entries since round 5): model.py Div -> Erf -> Add -> Mul ->
  * Mul on f32 (numpy_helper.py:95-112 erf) followed by numpy_quantization.py:24-34 quantize
  * with (s_out, zp_out, bit_width), as a step function of the dequantized, biased f32 value h:
- * at most 1024 buckets of 8 bytes in lut (an 8 KiB, 16-byte aligned device buffer), the bucket
+ * at most 1024 buckets of 8 bytes in lut (a 16-byte aligned device buffer of nqk_gelu_lut_capacity()
+ * bytes: 8 KiB since round 5, 4 KiB in round 4 — size it by the call, not a constant), the bucket
  * coordinate in k_out[5], the entry count in *n_out (the 128 x 256-tile k_pg takes tables of up
  * to 512 entries, the 256 x 256 one up to 1024; the builder prefers <= 512).  Every entry comes from the exact chain,
  * and the table is then compared with the exact chain on all 2^32 - 2^24 finite f32 inputs:
@@ -298,6 +299,9 @@ int nqk_pack_pg4(const int8_t* bt, uint8_t* out, int64_t N, int64_t K, int64_t l
  * 2..8.  Blocking (plan build time). */
 int nqk_gelu_lut_build(float s_out, int64_t zp_out, int32_t bit_width, float div, float add1, float mul2, void* lut,
                        float* k_out, int32_t* n_out);
+/* Bytes nqk_gelu_lut_build may write to its lut buffer (the API version check of the table
+ * size; k_pg itself reads only the 8 * lut_n bytes of the table it is given). */
+int nqk_gelu_lut_capacity(void);
 /* The number of finite f32 inputs on which a table (n entries, coordinate k) differs from the
  * exact chain (tests). */
 int nqk_gelu_lut_check(float s_out, int64_t zp_out, int32_t bit_width, float div, float add1, float mul2,

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sched.h>
 #include <time.h>
 
 #include "nqk_common.h"
@@ -25,14 +26,32 @@ double now_s() {
 // before joining does not wait forever inside ncclCommInitRank: every call returns
 // ncclInProgress until its host-side work is done, polled here against a deadline
 // (NQK_COMM_TIMEOUT_S, default 120 s); past it the communicator is aborted and the call fails.
+// The deadline covers the HOST side of a call (init, the enqueue of a collective).  A collective
+// already enqueued on the stream whose peer then dies never completes on the GPU: nqk_comm_barrier
+// (the only place this library waits for one) therefore polls the stream and the communicator's
+// async error against the same deadline instead of blocking in hipStreamSynchronize.  A caller that
+// synchronizes the stream itself (nqk_sync) is not covered: bench.py's parent kills such a rank.
 double comm_deadline_s() {
   const char* v = getenv("NQK_COMM_TIMEOUT_S");
   const double d = v ? atof(v) : 120.0;
   return d > 0 ? d : 120.0;
 }
+// a polling loop's pause: the first 2 000 polls spin (sched_yield), so a grouped op that reports
+// ncclInProgress for a few microseconds (ncclGather on a non-blocking communicator, every step)
+// does not pay a timer slice; past that 0.2 ms sleeps (the sleep alone cost a step
+// >= 0.2 ms)
+void pause_after(long spins) {
+  if (spins < 2000) {
+    sched_yield();
+  } else {
+    timespec ts{0, 200000};  // 0.2 ms
+    nanosleep(&ts, nullptr);
+  }
+}
 int nccl_wait(ncclResult_t r, const char* what) {
   if (r != ncclSuccess && r != ncclInProgress) return nccl_check(r, what);
   const double t0 = now_s(), lim = comm_deadline_s();
+  long spins = 0;
   while (r == ncclInProgress) {
     if (ncclCommGetAsyncError(g_comm, &r) != ncclSuccess) break;
     if (r != ncclInProgress) break;
@@ -42,8 +61,7 @@ int nccl_wait(ncclResult_t r, const char* what) {
       return nqk::fail(std::string(what) + ": not complete after " + std::to_string((int)lim) +
                        " s (a peer rank is gone?); communicator aborted");
     }
-    timespec ts{0, 200000};  // 0.2 ms
-    nanosleep(&ts, nullptr);
+    pause_after(++spins);
   }
   return nccl_check(r, what);
 }
@@ -91,7 +109,24 @@ int nqk_comm_barrier(void) {
   if (!scratch && nqk::check(hipMalloc(&scratch, 16), "hipMalloc")) return -1;
   if (nccl_wait(ncclAllReduce(scratch, scratch, 1, ncclInt32, ncclSum, g_comm, nqk::stream()), "ncclAllReduce"))
     return -1;
-  return nqk::check(hipStreamSynchronize(nqk::stream()), "hipStreamSynchronize");
+  // the stream drains when every rank joined the all-reduce: poll it (and the communicator's
+  // async error) against the deadline rather than block forever on a dead peer
+  const double t0 = now_s(), lim = comm_deadline_s();
+  for (long spins = 0;; ++spins) {
+    const hipError_t q = hipStreamQuery(nqk::stream());
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return nqk::check(q, "hipStreamQuery");
+    ncclResult_t ar = ncclSuccess;
+    if (ncclCommGetAsyncError(g_comm, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress)
+      return nccl_check(ar, "nqk_comm_barrier");
+    if (now_s() - t0 > lim) {
+      ncclCommAbort(g_comm);
+      g_comm = nullptr;
+      return nqk::fail("nqk_comm_barrier: the all-reduce did not complete after " + std::to_string((int)lim) +
+                       " s (a peer rank is gone?); communicator aborted");
+    }
+    pause_after(spins);
+  }
 }
 
 int nqk_comm_destroy(void) {

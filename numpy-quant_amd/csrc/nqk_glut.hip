@@ -122,6 +122,8 @@ double gelu_solve(double a, double b, double y) {
 
 }  // namespace
 
+extern "C" int nqk_gelu_lut_capacity(void) { return 8 * GLUT_MAX; }
+
 // Build the table for one GELU epilogue (nqk.h).  The bucket grid comes from double-precision
 // GELU (sizing only); every entry comes from the exact f32 chain on the device, and the whole
 // table is then compared with that chain on all finite f32 inputs.

@@ -174,6 +174,7 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   e.mul2 = p->mul2;
   e.ldo = (int)N;
   e.lut = glut ? p->gelu_lut : nullptr;
+  e.lut_bytes = glut ? (uint32_t)((8 * p->lut_n + 15) & ~15) : 0u;
   e.gk = GLutK{p->lut_k[0], p->lut_k[1], p->lut_k[2], p->lut_k[3], p->lut_k[4]};
   if (epi == PG_GELU) {
     // the GELU filter of nqk_fused.hip make_epi: |gelu_fast - gelu| <= GELU_REL |h| +

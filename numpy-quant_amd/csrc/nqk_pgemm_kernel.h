@@ -226,6 +226,7 @@ struct PgEpi {
   double rdiv;
   int ldo;  // row stride (elements) of the GELU / RESID output
   const void* lut;  // PG_GLUT: the GELU table (nqk_gelu_lut_build) and its bucket coordinate
+  uint32_t lut_bytes;  // 8 * lut_n rounded up to 16: the table's buffer range
   GLutK gk;
   float blo, bhi;   // QKV: the clamp of v + 128 ([lo + 128, hi + 128] of the bit width)
 };
@@ -871,7 +872,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     // VMEM operations per wave, in issue order: [B pieces when the panel changes], colp(next),
     // the next tile's A pieces (3 k steps), then the epilogue's EOPS stores: waiting for all but
     // EOPS waits for everything the next tile reads
-    if constexpr (pg_is_glut(EPI)) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
+    if constexpr (pg_is_glut(EPI)) pg_dma16(pg_rsrc(e.lut, e.lut_bytes), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
     auto issue_b = [&](const Src& s) __attribute__((always_inline)) {
 #pragma unroll
       for (int kt = 0; kt < NK; ++kt)
@@ -945,7 +946,9 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   }
   // PG_GLUT: the 4 KiB GELU table into LDS, 1 KiB per wave (waited for with stage 0)
   // (WM = 2: the 8 KiB of a table of up to GLUT_MAX entries, 1 KiB per wave as well)
-  if constexpr (pg_is_glut(EPI)) pg_dma16(pg_rsrc(e.lut, 8 * GLUT_MAX), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
+  // (the descriptor's range is the table's own 8 * lut_n bytes, rounded up to 16: the pieces past it
+  // read zeros, so a caller's buffer of exactly the table's size is never over-read)
+  if constexpr (pg_is_glut(EPI)) pg_dma16(pg_rsrc(e.lut, e.lut_bytes), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
   issue_colp(cur.tn, 0);
   sfor<0, RD - 1>([&](auto S) __attribute__((always_inline)) { issue_stage(cur, decltype(S)::value, decltype(S)::value); });
   if constexpr (NQK_PG_PRIO == 2) {

@@ -102,6 +102,7 @@ SIGNATURES = {
     "nqk_qgemm_last_kernel": [],
     "nqk_pack_pg4": [_p, _p, _l, _l, _l, _i],
     "nqk_gelu_lut_build": [_f, _l, _i, _f, _f, _f, _p, ctypes.POINTER(_f), ctypes.POINTER(ctypes.c_int32)],
+    "nqk_gelu_lut_capacity": [],
     "nqk_gelu_lut_check": [_f, _l, _i, _f, _f, _f, _p, ctypes.POINTER(_f), ctypes.c_int32,
                            ctypes.POINTER(ctypes.c_uint64)],
     "nqk_ln_quant": [_p, _p, _p, _p, _l, _l, _f, _f, _l, _i],

@@ -827,7 +827,7 @@ def _gelu_lut(p, bit_width, div, add1, mul2):
     the filtered chain) or NQK_NO_GLUT is set."""
     if os.environ.get("NQK_NO_GLUT") or p.zero_point is None or not hasattr(_lib.load(), "nqk_gelu_lut_build"):
         return None
-    lut = DeviceArray((8192,), np.uint8)
+    lut = DeviceArray((int(_lib.load().nqk_gelu_lut_capacity()),), np.uint8)  # the builder's own size
     k = (ctypes.c_float * 5)()
     n = ctypes.c_int32(0)
     _lib.call("nqk_gelu_lut_build", _f32(p.scale), int(p.zero_point), int(bit_width), _f32(div), _f32(add1),

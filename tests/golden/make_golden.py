@@ -3,7 +3,7 @@
 
 Runs only in the build container, where /root/reference exists (read-only).  The
 reference never travels: only the .npz/.json vectors this script writes are
-committed.  Usage:  python tests/golden/make_golden.py [--vit]
+committed.  Usage:  python tests/golden/make_golden.py [--vit] [--only l1,mlp,attn,layer,api,vit,vit4]
 
 How the reference is imported:
   * numpy_quant.numpy_quantization / .tensor / .numpy_helper are pure NumPy and
@@ -387,6 +387,10 @@ def main():
         gen_api(HERE)
     if args.vit or (only and "vit" in only):
         gen_vit_part(HERE, "vit_image_classifier_no_weights.onnx", "vit_b1", 1, bit_widths=(8,), keep_small=False)
+    if only and "vit4" in only:
+        # configs[4] pinned at the full-classifier level (VERDICT r5 missing #3): the reference's own
+        # Model.quantize(bit_width=4) + QModel.__call__ on the same seeded graph and images as vit_b1
+        gen_vit_part(HERE, "vit_image_classifier_no_weights.onnx", "vit_b1_bw4", 1, bit_widths=(4,), keep_small=False)
 
 
 if __name__ == "__main__":

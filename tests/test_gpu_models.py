@@ -127,6 +127,9 @@ def tainted_values(model):
     ("attn_b2", "vit_image_classifier_self_attention_no_weights.onnx", 2),
     ("layer_b1", "vit_image_classifier_encoder_layer_no_weights.onnx", 1),
     ("vit_b1", "vit_image_classifier_no_weights.onnx", 1),
+    # configs[4] at the full-classifier level: the reference's Model.quantize(bit_width=4) +
+    # QModel.__call__ (round 6, tests/golden/make_golden.py --only vit4)
+    ("vit_b1_bw4", "vit_image_classifier_no_weights.onnx", 1),
 ])
 def test_vit_graphs_bit_exact(tag, fname, batch):
     from numpy_quant import onnx_proto
