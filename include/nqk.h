@@ -257,6 +257,17 @@ typedef struct nqk_epilogue {
                                         /* (0: unknown); |acc| <= 2^(bw-1) col_l1max then  */
                                         /* bounds the f32-exactness test more tightly than */
                                         /* 2^(2bw-2) K (FFN-down at K = 3072)              */
+  /* optional (EPI_RESID, round 6): the consumer LayerNormalization (model.py:134-152) fused
+   * into the epilogue, quantized for ITS consumer MatMul (numpy_quantization.py:24-34):
+   * ln_out [M][N] int8 = quantize(LN(y) * ln_gamma + ln_beta, ln_scale, ln_zp, bit_width) of
+   * the f32 rows y the epilogue writes to out[0].  Whole rows per tile: N = 192 only (NumPy's
+   * pairwise tree of two 96-column leaves, the ViT-Ti width); anything else fails.  Bit-identical
+   * to nqk_ln_quant on out[0].  NULL: no LayerNorm. */
+  const float* ln_gamma;
+  const float* ln_beta;
+  int8_t* ln_out;
+  float ln_eps, ln_scale;
+  int64_t ln_zp;
 } nqk_epilogue;
 /* int8 MFMA GEMM C = A . Bt^T (layouts as nqk_qgemm_i8) with a fused epilogue:
  *   QKV    model.py MatMul -> Add(bias) -> Reshape -> Transpose -> quantize, 3 groups

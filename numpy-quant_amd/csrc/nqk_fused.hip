@@ -54,6 +54,33 @@ __device__ __forceinline__ int quant_zp(float x, float s, double rs, double zp, 
   return (int)__builtin_rint(qclip(u, lo, hi));
 }
 
+// LayerNorm output quantize (numpy_quantization.py:24-34): t = RN32(RN64(y rs)) exactly as the
+// reference's f64 product, then q = rint(clip(zp + t, lo, hi)) by the magic number instead of
+// f64 arithmetic (round 5): c = med3(t, lo - zp, hi - zp) clamps in t's space (integer bounds:
+// the same as clamping zp + t), and RN32(c + 1.5 2^23 + zp) lies in [2^23, 2^24), where the f32
+// spacing is 1, so it is rint(c + zp) with ties to even (1.5 2^23 is even) — the low byte of its
+// bits is the output byte.  Exact for |zp| <= 2^20 and bit widths <= 8 (host-checked, LNQ);
+// 3 f32 + 2 f64-rate instructions per element instead of 9 mostly f64-rate ones.
+struct LnQ {
+  float qlo, qhi, magic;
+};
+template <bool PK = false>
+__device__ __forceinline__ uint32_t ln_quant4(const float (&y)[4], double rs, const LnQ& m) {
+  float sv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sv[k] = __builtin_amdgcn_fmed3f((float)((double)y[k] * rs), m.qlo, m.qhi);
+  if constexpr (PK) {  // the magic-number adds as two packed pairs
+    const v2f_t s01 = v2f_t{sv[0], sv[1]} + v2f_t{m.magic, m.magic}, s23 = v2f_t{sv[2], sv[3]} + v2f_t{m.magic, m.magic};
+    sv[0] = s01[0], sv[1] = s01[1], sv[2] = s23[0], sv[3] = s23[1];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sv[k] = sv[k] + m.magic;
+  }
+  const uint32_t x01 = __builtin_amdgcn_perm(__float_as_uint(sv[1]), __float_as_uint(sv[0]), 0x0c0c0400u);
+  const uint32_t x23 = __builtin_amdgcn_perm(__float_as_uint(sv[3]), __float_as_uint(sv[2]), 0x04000c0cu);
+  return x01 | x23;
+}
+
 struct Epi {
   // zero-point term (see nqk.h): zpt = rowsumA[m]*zpb + rowsumBt[n]*zpa - zpa*zpb*K; the
   // row sums of A and of Bt are accumulated inside the kernel from the staged tiles
@@ -79,6 +106,14 @@ struct Epi {
   float g_rel, g_abs, g_lim;  // GELU filter error terms, in units of t; g_lim = (0.5 - g_abs) rounded down
   int b_packed;              // Bt is the tile-packed image of nqk_pack_b
   const int32_t* colterm;    // int32 col * zpa (k_proj), or null
+  // EPI_RESID with the consumer LayerNorm fused (nqk_epilogue.ln_out, round 6; k_qgemm_big<LN>)
+  const float* ln_g;
+  const float* ln_b;
+  int8_t* ln_out;
+  float ln_eps;
+  int ln_mq;                 // 1: the magic-number output quantize (exact, host-checked as nqk_ln_quant's)
+  double ln_rs, ln_zp, ln_lo, ln_hi;
+  LnQ ln_q;
 };
 
 enum { EPI_QKV = 0, EPI_SCORES = 1, EPI_PV = 2, EPI_RESID = 3, EPI_GELU = 4, EPI_NULL = 5 };
@@ -558,16 +593,46 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((c
 // loop): each wave owns a G_RP x 72-int32 slice; 128 / G_RP passes of G_RP rows.  Read
 // back row-major, a lane takes 4 consecutive columns of one row, so bias / column terms
 // are per lane and the outputs leave as 4-byte (int8) or 16-byte (f32) stores.
-template <int EPI, bool I32, bool F32X, int ASH = 0>
+// LN (EPI_RESID, N = 192 = two NumPy leaves of 96: ViT-Ti; round 6): the consumer LayerNorm of every
+// output row, fused.  Each pass's 32 rows of y go, besides their f32 stores, into a row image in LDS
+// (after the four waves' staging slices; leaf 1 shifted by 16 floats and rows LN_IMGS floats apart,
+// so the tree reads below hit 32 different banks per lane group), then — after a workgroup barrier —
+// all four waves (wave 3 holds no columns at N = 192) normalize 8 rows each, 4 at a time with 16
+// lanes per row: lane (row, leaf, j) sums NumPy's accumulator j of its leaf (columns leaf 96 + 8 i + j,
+// in increasing i), the ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) combine and the leaf sum
+// are xor butterflies 1, 2, 4, 8 (float addition commutes; only the grouping matters) — the same
+// IEEE operations in the same order as k_ln_quant_lds<2> on the rows this kernel just wrote; then
+// each lane normalizes, scales and quantizes 12 contiguous columns and stores them as 12 bytes.
+constexpr int LN_IMGS = 232;  // floats per image row: 192 + 16 (leaf shift) + 24; 232 = 8 mod 32
+__device__ __forceinline__ int ln_ipos(int c) { return c + (c >= 96 ? 16 : 0); }
+template <int CTRL>  // v of another lane of the 16-lane row (DPP: no LDS round trip)
+__device__ __forceinline__ float ln_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int EPI, bool I32, bool F32X, int ASH = 0, bool LN = false>
 __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], const Epi& e, int mw, int ncol0,
                                               int M, int N, int wave, int lane) {
   constexpr int RP = G_RP;
+  static_assert(!LN || EPI == EPI_RESID, "proj_epilogue: the LayerNorm fuses into the residual epilogue");
   const int r32 = lane & 31, half = lane >> 5;
   int32_t* stg = reinterpret_cast<int32_t*>(lds) + wave * (RP * 72);
+  float* const lnimg = reinterpret_cast<float*>(lds + 4 * RP * 72 * 4);  // LN: the pass's 32 rows of y
   const int c4 = (lane & 15) * 4;
   const int gn0 = ncol0 + c4;
   const bool cok = gn0 < N;  // N % 4 == 0 (host-checked): the 4 columns are valid together
   EpiCol4 cc = epi_col4<EPI>(e, gn0, cok);
+  // LN: this lane's 12 contiguous columns 12 c16 .. (gamma, beta), the same in every row
+  float lg[12], lb[12];
+  if constexpr (LN) {
+    const int c12 = 12 * (lane & 15);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float4 g4 = *reinterpret_cast<const float4*>(e.ln_g + c12 + 4 * k);
+      const float4 b4 = *reinterpret_cast<const float4*>(e.ln_b + c12 + 4 * k);
+      lg[4 * k] = g4.x, lg[4 * k + 1] = g4.y, lg[4 * k + 2] = g4.z, lg[4 * k + 3] = g4.w;
+      lb[4 * k] = b4.x, lb[4 * k + 1] = b4.y, lb[4 * k + 2] = b4.z, lb[4 * k + 3] = b4.w;
+    }
+  }
   // residual rows: pass 0's in flight while its tile is staged, every later pass's
   // issued right after the previous pass is staged (two register sets; the staged
   // accumulators of earlier passes are dead by then)
@@ -608,7 +673,107 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
         while (t >= e.tokens) { t -= e.tokens; ++img; }
       }
     };
-    if constexpr (EPI == EPI_RESID) {
+    if constexpr (LN) {
+      // the residual rows as in epi_row4, and each row of y also into the LDS image
+#pragma unroll
+      for (int it = 0; it < RP / 4; ++it) {
+        const v4i a4 = row_acc(it);
+        const float4 r4 = rv[pass & 1][it];
+        float4 y;
+        y.x = (cc.bias[0] + dequant_elem<I32>(a4[0], cc.colterm[0], cc.s_acc)) + r4.x;
+        y.y = (cc.bias[1] + dequant_elem<I32>(a4[1], cc.colterm[1], cc.s_acc)) + r4.y;
+        y.z = (cc.bias[2] + dequant_elem<I32>(a4[2], cc.colterm[2], cc.s_acc)) + r4.z;
+        y.w = (cc.bias[3] + dequant_elem<I32>(a4[3], cc.colterm[3], cc.s_acc)) + r4.w;
+        if (gm < M && cok) *reinterpret_cast<float4*>((float*)e.out[0] + (int64_t)gm * N + cc.dd) = y;
+        if (cok) *reinterpret_cast<float4*>(lnimg + (it * 4 + (lane >> 4)) * LN_IMGS + ln_ipos(gn0)) = y;
+        gm += 4;
+      }
+      __syncthreads();  // the pass's 32 rows of y are in the image
+      const int jr = lane >> 4, leaf = (lane >> 3) & 1, j = lane & 7, c16 = lane & 15;
+      // the wave's 8 rows as two independent groups of 4 (their chains interleave); the butterfly
+      // steps by DPP inside each 16-lane row: after step 1 the values are uniform per lane pair, after
+      // step 2 per quad, after step 3 per leaf, so quad_perm [1,0,3,2], quad_perm [2,3,0,1],
+      // row_half_mirror and row_mirror pair exactly the NumPy partners (xor 1, 2, 4, 8)
+      float xv[2][12], nmean[2], inv[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const float* irow = lnimg + (8 * wave + 4 * h2 + jr) * LN_IMGS;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) xv[h2][i] = irow[ln_ipos(leaf * 96 + 8 * i + j)];
+      }
+      auto tree16 = [&](float a) __attribute__((always_inline)) {
+        a = a + ln_dpp<0xB1>(a);
+        a = a + ln_dpp<0x4E>(a);
+        a = a + ln_dpp<0x141>(a);
+        return a + ln_dpp<0x140>(a);
+      };
+      {
+        float s0 = xv[0][0], s1 = xv[1][0];
+#pragma unroll
+        for (int i = 1; i < 12; ++i) {
+          s0 = s0 + xv[0][i];
+          s1 = s1 + xv[1][i];
+        }
+        s0 = tree16(s0);
+        s1 = tree16(s1);
+        nmean[0] = -(s0 / 192.0f);
+        nmean[1] = -(s1 / 192.0f);
+      }
+      {
+        float v0, v1;
+        {
+          const float d0 = xv[0][0] + nmean[0], d1 = xv[1][0] + nmean[1];
+          v0 = d0 * d0;
+          v1 = d1 * d1;
+        }
+#pragma unroll
+        for (int i = 1; i < 12; ++i) {
+          const float d0 = xv[0][i] + nmean[0], d1 = xv[1][i] + nmean[1];
+          v0 = v0 + d0 * d0;
+          v1 = v1 + d1 * d1;
+        }
+        v0 = tree16(v0);
+        v1 = tree16(v1);
+        inv[0] = 1.0f / __builtin_sqrtf(v0 / 192.0f + e.ln_eps);
+        inv[1] = 1.0f / __builtin_sqrtf(v1 / 192.0f + e.ln_eps);
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int rr = 8 * wave + 4 * h2 + jr;  // row of the pass
+        // normalize + affine + quantize 12 contiguous columns (inside one leaf: 96 = 8 x 12)
+        const float* src = lnimg + rr * LN_IMGS + ln_ipos(12 * c16);
+        uint32_t pk[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float4 x4 = *reinterpret_cast<const float4*>(src + 4 * k);
+          const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+          float yv[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) yv[q] = (((xs[q] + nmean[h2]) * inv[h2]) * lg[4 * k + q]) + lb[4 * k + q];
+          if (e.ln_mq) {
+            pk[k] = ln_quant4(yv, e.ln_rs, e.ln_q);
+          } else {
+            uint32_t w = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float t = (float)((double)yv[q] * e.ln_rs);
+              const double uu = e.ln_zp + (double)t;
+              const int qv = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, e.ln_lo), e.ln_hi));
+              w |= ((uint32_t)(qv & 0xff)) << (8 * q);
+            }
+            pk[k] = w;
+          }
+        }
+        const int grow = mw + pass * RP + rr;
+        if (grow < M) {
+          uint32_t* o = reinterpret_cast<uint32_t*>(e.ln_out + (int64_t)grow * 192 + 12 * c16);
+          o[0] = pk[0];
+          o[1] = pk[1];
+          o[2] = pk[2];
+        }
+      }
+      __syncthreads();  // every wave has read the image: the next pass may overwrite it
+    } else if constexpr (EPI == EPI_RESID) {
 #pragma unroll
       for (int it = 0; it < RP / 4; ++it) row_step(row_acc(it), rv[pass & 1][it]);
     } else {
@@ -661,7 +826,7 @@ __device__ __forceinline__ void tile_of(int wg, int tiles_m, int tiles_n, int& t
 // bytes 16 * w (the nibble lands in the high half, its sign bit on the byte's): the
 // MFMA then accumulates 16 * acc exactly (|acc| <= 2^11 K), and the epilogue takes
 // acc >> 4.
-template <int EPI, bool I32, bool F32X, bool B4 = false>
+template <int EPI, bool I32, bool F32X, bool B4 = false, bool LN = false>
 __global__ void __launch_bounds__(256, 2)
 k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, int N, int K, int lda, int ldb,
             int tiles_m, int tiles_n, Epi e) {
@@ -824,7 +989,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   kstep(nk - 1, S2{}, F_{}, T_{});
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  proj_epilogue<EPI, I32, F32X, B4 ? 4 : 0>(lds, acc, e, m0, n0 + wn * 64, M, N, wave, lane);
+  proj_epilogue<EPI, I32, F32X, B4 ? 4 : 0, LN>(lds, acc, e, m0, n0 + wn * 64, M, N, wave, lane);
 }
 
 template <int EPI, bool I32, bool F32X>
@@ -1519,33 +1684,6 @@ k_ln_quant(const float* __restrict__ x, const float* __restrict__ g, const float
 // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) combine and the leaf tree are xor-butterflies
 // (float addition is commutative, only the grouping matters).  2*NL lanes per row,
 // 64 / (2*NL) rows per wave; every load and store is 16 / 4 bytes per lane.
-// LayerNorm output quantize (numpy_quantization.py:24-34): t = RN32(RN64(y rs)) exactly as the
-// reference's f64 product, then q = rint(clip(zp + t, lo, hi)) by the magic number instead of
-// f64 arithmetic (round 5): c = med3(t, lo - zp, hi - zp) clamps in t's space (integer bounds:
-// the same as clamping zp + t), and RN32(c + 1.5 2^23 + zp) lies in [2^23, 2^24), where the f32
-// spacing is 1, so it is rint(c + zp) with ties to even (1.5 2^23 is even) — the low byte of its
-// bits is the output byte.  Exact for |zp| <= 2^20 and bit widths <= 8 (host-checked, LNQ);
-// 3 f32 + 2 f64-rate instructions per element instead of 9 mostly f64-rate ones.
-struct LnQ {
-  float qlo, qhi, magic;
-};
-template <bool PK = false>
-__device__ __forceinline__ uint32_t ln_quant4(const float (&y)[4], double rs, const LnQ& m) {
-  float sv[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) sv[k] = __builtin_amdgcn_fmed3f((float)((double)y[k] * rs), m.qlo, m.qhi);
-  if constexpr (PK) {  // the magic-number adds as two packed pairs
-    const v2f_t s01 = v2f_t{sv[0], sv[1]} + v2f_t{m.magic, m.magic}, s23 = v2f_t{sv[2], sv[3]} + v2f_t{m.magic, m.magic};
-    sv[0] = s01[0], sv[1] = s01[1], sv[2] = s23[0], sv[3] = s23[1];
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) sv[k] = sv[k] + m.magic;
-  }
-  const uint32_t x01 = __builtin_amdgcn_perm(__float_as_uint(sv[1]), __float_as_uint(sv[0]), 0x0c0c0400u);
-  const uint32_t x23 = __builtin_amdgcn_perm(__float_as_uint(sv[3]), __float_as_uint(sv[2]), 0x04000c0cu);
-  return x01 | x23;
-}
-
 #ifndef NQK_LN_LB
 #define NQK_LN_LB 1
 #endif
@@ -2039,6 +2177,18 @@ template <int EPI, bool I32, bool F32X>
 static void launch_big(bool pp, const int8_t* a, const int8_t* bt, int64_t M, int64_t N, int64_t K, int64_t lda,
                        int64_t ldb, const Epi& e) {
   const int tn = (int)((N + GBN - 1) / GBN);
+  if constexpr (EPI == EPI_RESID && !F32X) {
+    if (e.ln_out != nullptr) {  // the consumer LayerNorm fused (N = 192, host-checked)
+      const int tm = (int)((M + 127) / 128);
+      if (e.b_packed == 2)
+        hipLaunchKernelGGL((k_qgemm_big<EPI, I32, F32X, true, true>), dim3(tm * tn), dim3(256), BIG_LDS, stream(), a,
+                           bt, (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e);
+      else
+        hipLaunchKernelGGL((k_qgemm_big<EPI, I32, F32X, false, true>), dim3(tm * tn), dim3(256), BIG_LDS, stream(), a,
+                           bt, (int)M, (int)N, (int)K, (int)lda, (int)ldb, tm, tn, e);
+      return;
+    }
+  }
   if constexpr (I32 && EPI != EPI_NULL) {
     if (e.b_packed == 2) {  // int4 nibble image (nqk_pack_b4)
       const int tm = (int)((M + 127) / 128);
@@ -2141,6 +2291,20 @@ static Epi make_epi(const nqk_epilogue* p) {
   e.colterm = p->colterm;
   e.lof = (float)e.lo;
   e.hif = (float)e.hi;
+  e.ln_g = p->ln_gamma;
+  e.ln_b = p->ln_beta;
+  e.ln_out = p->ln_out;
+  e.ln_eps = p->ln_eps;
+  if (p->ln_out != nullptr) {
+    e.ln_rs = 1.0 / (double)p->ln_scale;
+    e.ln_zp = (double)p->ln_zp;
+    e.ln_lo = e.lo;
+    e.ln_hi = e.hi;
+    // nqk_ln_quant's conditions for the magic-number quantize (NQK_LN_F64Q=1 keeps the f64 chain)
+    e.ln_mq = p->bit_width >= 1 && p->bit_width <= 8 && p->ln_zp >= -(1 << 20) && p->ln_zp <= (1 << 20) &&
+              !getenv("NQK_LN_F64Q");
+    e.ln_q = LnQ{(float)(e.lo - (double)p->ln_zp), (float)(e.hi - (double)p->ln_zp), 0x1.8p23f + (float)p->ln_zp};
+  }
   return e;
 }
 
@@ -2197,6 +2361,15 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
   if (epi == EPI_GELU) scales_ok = scales_ok && normal(params->div);
   if (params->b_packed == 2 && (!i32 || epi == EPI_NULL))
     return fail("nqk_qgemm_fused: int4 packed weights need the int32 zero-point algebra");
+  if (params->ln_out != nullptr) {
+    // the fused LayerNorm: the one-tile-per-workgroup kernel with whole 192-column rows per tile
+    if (!(epi == EPI_RESID && N == 192 && big && aligned && params->ln_gamma && params->ln_beta &&
+          (((uintptr_t)params->ln_gamma | (uintptr_t)params->ln_beta) & 15) == 0 && (((uintptr_t)params->ln_out) & 3) == 0 &&
+          __builtin_fabsf(params->ln_scale) >= 0x1p-100f && __builtin_fabsf(params->ln_scale) <= 0x1p100f &&
+          !pp && !getenv("NQK_PROJ_RESID")))
+      return fail("nqk_qgemm_fused: a fused LayerNorm needs the residual epilogue at N = 192 on the big-tile path "
+                  "(16-byte aligned gamma / beta, a normal ln_scale)");
+  }
   if (params->b_packed && !(big && aligned && scales_ok && (K % (GST * GBK)) == 0))
     return fail("nqk_qgemm_fused: a packed B operand needs the big-tile path (K % 192 == 0, N % 4 == 0, "
                 "COL zero-point term, aligned outputs)");
@@ -2215,8 +2388,9 @@ extern "C" int nqk_qgemm_fused(int epi, const int8_t* a, const int8_t* bt, int64
     const bool f32x = i32 && (epi == EPI_QKV || (epi == EPI_GELU && e.gelu_filter)) && zp_small &&
                       abound + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
     const bool use_pp = pp && !params->b_packed;
-    // the persistent 16x16x64 GEMM (nqk_pgemm.hip) where it takes the case
-    if (params->bt_pg != nullptr) {
+    // the persistent 16x16x64 GEMM (nqk_pgemm.hip) where it takes the case (never with a fused
+    // LayerNorm: its residual epilogue needs whole 256-column tiles)
+    if (params->bt_pg != nullptr && params->ln_out == nullptr) {
       const bool f32x_r = i32 && epi == EPI_RESID && abound + cmax * za < 16777216.0 && !getenv("NQK_NO_F32X");
       const int rc = pg_launch(epi, a, params->bt_pg, M, N, K, lda, params, f32x || f32x_r);
       if (rc < 0) return rc;

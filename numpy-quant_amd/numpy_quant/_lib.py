@@ -35,7 +35,9 @@ class Epilogue(ctypes.Structure):
                 ("div", ctypes.c_float), ("add1", ctypes.c_float), ("mul2", ctypes.c_float),
                 ("b_packed", ctypes.c_int32), ("colterm", ctypes.c_void_p), ("bt_pg", ctypes.c_void_p),
                 ("gelu_lut", ctypes.c_void_p), ("lut_k", ctypes.c_float * 5), ("lut_n", ctypes.c_int32),
-                ("col_l1max", ctypes.c_int32)]
+                ("col_l1max", ctypes.c_int32),
+                ("ln_gamma", ctypes.c_void_p), ("ln_beta", ctypes.c_void_p), ("ln_out", ctypes.c_void_p),
+                ("ln_eps", ctypes.c_float), ("ln_scale", ctypes.c_float), ("ln_zp", ctypes.c_int64)]
 
 
 class Attention(ctypes.Structure):

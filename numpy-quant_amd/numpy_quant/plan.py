@@ -631,6 +631,13 @@ class FusedLayer:
         zs = [_zp(self.p_head["q"]), _zp(self.p_head["k"]), _zp(self.p_sm), _zp(self.p_head["v"])]
         self.attn_fused = (FUSED_ATTENTION and m.hdim == 64 and 1 <= m.tokens <= 224 and
                            abs(zs[0]) <= 4096 and abs(zs[1]) <= 4096 and abs(zs[2]) <= 1024 and abs(zs[3]) <= 1024)
+        # round 6: at width 192 (ViT-Ti) a residual GEMM tile holds whole rows, so the LayerNorm that
+        # reads its output (LN2 after the out-projection; the NEXT layer's LN1 after FFN-down, linked
+        # by the Plan) runs inside its epilogue (nqk_epilogue.ln_out): 24 LayerNorm launches and their
+        # f32 row reads fewer per forward.  NQK_NO_LNFUSE=1 keeps the separate launches.
+        self.ln_fuse = self.D == 192 and not os.environ.get("NQK_NO_LNFUSE")
+        self.next_ln = None        # the next fused layer, whose LN1 this layer's FFN-down computes
+        self.ln1_by_prev = False   # this layer's LN1 is computed by the previous layer's FFN-down
 
     def _epi(self, **kw) -> Epilogue:
         e = Epilogue()
@@ -646,6 +653,13 @@ class FusedLayer:
             else:
                 setattr(e, k, v)
         return e
+
+    @staticmethod
+    def _ln_into(e, g, b, eps, p, out):
+        """Fuse the LayerNorm (gamma g, beta b, epsilon eps) of the residual epilogue's output rows,
+        quantized with p, into e (nqk_epilogue.ln_*): out gets what nqk_ln_quant would write."""
+        e.ln_gamma, e.ln_beta, e.ln_out = g.ptr, b.ptr, out.ptr
+        e.ln_eps, e.ln_scale, e.ln_zp = eps, _f32(p.scale), _zp(p)
 
     def _b(self, e, key, bt):
         """The B operand of a projection GEMM: its packed image if there is one (and the
@@ -727,8 +741,10 @@ class FusedLayer:
         hq = i0 * H * T * Dh  # head-layout offset of the first image
         q, k, v = (w[r].offset_view(hq, (nb * H * T, Dh)) for r in "qkv")
         call = _lib.call
-        # 1) LN1 + quantize (LN1 output feeds the Q/K/V MatMuls)
-        _ln_quant(x, self.g1, self.be1, lnq, Mrows, D, self.eps1, self.p_ln1, bw)
+        # 1) LN1 + quantize (LN1 output feeds the Q/K/V MatMuls; already in lnq when the previous
+        # layer's FFN-down epilogue computed it)
+        if not self.ln1_by_prev:
+            _ln_quant(x, self.g1, self.be1, lnq, Mrows, D, self.eps1, self.p_ln1, bw)
         mark("ln1")
         # 2) QKV projection: dequant + bias + head split + quantize with each head consumer's params
         s_a = np.float32(self.p_ln1.scale)
@@ -762,9 +778,11 @@ class FusedLayer:
                       colterm=_ptr(self.ct["o"]),
                       s_acc=[_f32(np.float32(self.p_ctx.scale) * np.float32(self.s_wo))], bias=self.bias_o.ptr,
                       resid=x.ptr, out=[x1.ptr])
+        if self.ln_fuse:  # 8) LN2 + quantize inside the epilogue
+            self._ln_into(e, self.g2, self.be2, self.eps2, self.p_ln2, ln2q)
         _gemm(EPI_RESID, ctx, self._b(e, "o", self.bt_o), 1, Mrows, D, D, D, D, None, 0, 0, e)
-        # 8) LN2 + quantize
-        _ln_quant(x1, self.g2, self.be2, ln2q, Mrows, D, self.eps2, self.p_ln2, bw)
+        if not self.ln_fuse:  # 8) LN2 + quantize
+            _ln_quant(x1, self.g2, self.be2, ln2q, Mrows, D, self.eps2, self.p_ln2, bw)
         # 9) FFN up + bias + GELU + quantize
         e = self._epi(zp_flags=_lib.ZP_COL, zpa=_zp(self.p_ln2), col=self.col_1.ptr, col_absmax=self.cmax["1"], col_l1max=self.l1max["1"],
                       colterm=_ptr(self.ct["1"]),
@@ -781,6 +799,9 @@ class FusedLayer:
                       colterm=_ptr(self.ct["2"]),
                       s_acc=[_f32(np.float32(self.p_h.scale) * np.float32(self.s_w2))], bias=self.bias_2.ptr,
                       resid=x1.ptr, out=[x2.ptr])
+        nl = self.next_ln
+        if nl is not None:  # the next layer's LN1 + quantize inside the epilogue, into the shared lnq rows
+            self._ln_into(e, nl.g1, nl.be1, nl.eps1, nl.p_ln1, lnq)
         _gemm(EPI_RESID, hh, self._b(e, "2", self.bt_2), 1, Mrows, D, F, F, F, None, 0, 0, e)
 
 
@@ -1022,6 +1043,13 @@ class Plan:
                 placed.add(id(layer))
                 self.steps.append(("layer", layer))
                 self.fused += 1
+        # consecutive fused layers of width 192: layer i's FFN-down epilogue computes layer i + 1's
+        # LN1 (the same workspace rows its QKV GEMM reads: equal layer dimensions)
+        for (k0, a), (k1, b) in zip(self.steps, self.steps[1:]):
+            if (k0 == "layer" and k1 == "layer" and a.ln_fuse and b.ln_fuse and b.m.x_in is a.m.x_out and
+                    (a.D, a.F, a.m.heads, a.m.hdim, a.m.tokens, a.attn_fused) ==
+                    (b.D, b.F, b.m.heads, b.m.hdim, b.m.tokens, b.attn_fused)):
+                a.next_ln, b.ln1_by_prev = b, True
         # every value a fused step computes; each run first marks them all FusedAway, so that
         # no tensor of an earlier run (eager, keep_values) can be read as if it were this
         # run's; the steps then set the values their consumers outside the step read

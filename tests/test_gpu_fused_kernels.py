@@ -363,3 +363,71 @@ def test_persistent_projection_gemm_equals_big_tile(epi_name, M, N, K, bw, monke
     for o in outs[1:]:
         for x, y in zip(outs[0], o):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("M,K", [(128 * 197, 192), (128 * 197, 768), (1000, 192), (131, 768), (256 * 197, 768)])
+@pytest.mark.parametrize("bw,zp,f64q", [(8, -5, False), (8, 140, False), (4, 2, False), (8, 3, True)])
+def test_resid_epilogue_fused_layernorm_equals_ln_quant(M, K, bw, zp, f64q, monkeypatch):
+    """Round 6: the residual GEMM's epilogue with the consumer LayerNorm fused
+    (nqk_epilogue.ln_out, k_qgemm_big<RESID, LN>, N = 192: ViT-Ti's out-projection K = 192 and FFN-down
+    K = 768) writes the same f32 rows as without it, and its int8 LayerNorm output equals nqk_ln_quant
+    run on those rows, bit for bit (ragged last tiles; the magic-number and the f64 quantize)."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_RESID, _gemm, _pack_b
+    if f64q:
+        monkeypatch.setenv("NQK_LN_F64Q", "1")
+    else:
+        monkeypatch.delenv("NQK_LN_F64Q", raising=False)
+    N = 192
+    rng = np.random.default_rng(M + K + bw + zp)
+    a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
+    bt_h = rng.integers(-30, 31, size=(N, K), dtype=np.int8)
+    bt = DeviceArray.from_host(bt_h)
+    col_h = bt_h.astype(np.int64).sum(axis=1)
+    col = DeviceArray.from_host(col_h)
+    bias = DeviceArray.from_host((0.05 * rng.standard_normal(N)).astype(np.float32))
+    resid = DeviceArray.from_host((rng.standard_normal((M, N)) * 1.5).astype(np.float32))
+    g = DeviceArray.from_host((1 + 0.1 * rng.standard_normal(N)).astype(np.float32))
+    b = DeviceArray.from_host((0.1 * rng.standard_normal(N)).astype(np.float32))
+    eps, s_ln = float(np.float32(1e-12)), float(np.float32(0.021 if bw == 8 else 0.4))
+    bp = _pack_b(bt, 8)
+    outs = []
+    for fuse in (False, True):
+        e = _lib.Epilogue()
+        e.zp_flags, e.bit_width, e.zpa, e.col, e.col_absmax = _lib.ZP_COL, bw, 7, col.ptr, int(np.abs(col_h).max())
+        e.bias, e.group_cols = bias.ptr, 1 << 30
+        e.b_packed = 0 if bp is None else bp[1]
+        y = DeviceArray((M, N), np.float32)
+        e.s_acc[0], e.out[0], e.resid = float(np.float32(2.3e-4)), y.ptr, resid.ptr
+        lnq = DeviceArray((M, N), np.int8)
+        if fuse:
+            e.ln_gamma, e.ln_beta, e.ln_out, e.ln_eps, e.ln_scale, e.ln_zp = g.ptr, b.ptr, lnq.ptr, eps, s_ln, zp
+        _gemm(EPI_RESID, a, bt if bp is None else bp[0], 1, M, N, K, K, K, None, 0, 0, e)
+        if fuse:
+            assert _last_kernel() == 1  # the one-tile-per-workgroup kernel
+        else:
+            _lib.call("nqk_ln_quant", y.vp, g.vp, b.vp, lnq.vp, M, N, eps, s_ln, zp, bw)
+        outs.append((y.to_host(), lnq.to_host()))
+    np.testing.assert_array_equal(outs[1][0], outs[0][0], err_msg="f32 residual rows")
+    np.testing.assert_array_equal(outs[1][1], outs[0][1], err_msg="fused LayerNorm vs nqk_ln_quant")
+
+
+def test_resid_fused_layernorm_refuses_other_widths():
+    """A fused LayerNorm at a width other than 192 fails loudly (no silent unfused path)."""
+    from numpy_quant import _lib
+    from numpy_quant.device import DeviceArray
+    from numpy_quant.plan import EPI_RESID, _gemm
+    M, N, K = 256, 768, 768
+    rng = np.random.default_rng(5)
+    a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
+    bt_h = rng.integers(-30, 31, size=(N, K), dtype=np.int8)
+    bt, col = DeviceArray.from_host(bt_h), DeviceArray.from_host(bt_h.astype(np.int64).sum(axis=1))
+    y, resid, lnq = DeviceArray((M, N), np.float32), DeviceArray((M, N), np.float32), DeviceArray((M, N), np.int8)
+    gb = DeviceArray.from_host(np.ones(N, np.float32))
+    e = _lib.Epilogue()
+    e.zp_flags, e.bit_width, e.zpa, e.col, e.group_cols = _lib.ZP_COL, 8, 1, col.ptr, 1 << 30
+    e.s_acc[0], e.out[0], e.resid = 1e-3, y.ptr, resid.ptr
+    e.ln_gamma, e.ln_beta, e.ln_out, e.ln_eps, e.ln_scale, e.ln_zp = gb.ptr, gb.ptr, lnq.ptr, 1e-12, 0.02, 0
+    with pytest.raises(_lib.NQKError, match="fused LayerNorm"):
+        _gemm(EPI_RESID, a, bt, 1, M, N, K, K, K, None, 0, 0, e)
