@@ -970,6 +970,318 @@ k_attention(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// k_attn16 (round 6): the T = 197 FAST attention on v_mfma_i32_16x16x64_i8, FOUR lanes per query
+// row (k_attention: 32x32x32, two lanes per row).  Why: k_attention holds a query's 112 scores per
+// lane (168 VGPRs: three waves per SIMD) and its waves sit 30 % dependency-stalled and 33 % parked
+// (profiles/r05_attn_diag.txt) — VALU-issue is 40 % busy.  Here a lane holds 52 scores (13 tiles of
+// 16 keys x 4): fewer registers, more waves per SIMD to hide the same chains; the key dimension pads
+// to 208 instead of 224 (7 % less exp / quantize work on pads); and the probabilities P feed the
+// P V MFMAs from the lane that computed them (no cross-lane exchange).
+//
+// Key order.  Score tile c, position p = 4 g + r (g = lane >> 4, the lane group; r the accumulator
+// register) holds key n(c, p) = 16 c + 8 (r >> 1) + 2 g + (r & 1): lane group g owns exactly NumPy's
+// pairwise accumulators j = 2 g and 2 g + 1 (keys n = j mod 8), so every accumulator chain runs
+// in-lane in increasing n (two tiles' t = 0, 1 halves in order), and the ((r0 + r1) + (r2 + r3)) +
+// ((r4 + r5) + (r6 + r7)) combine is an in-lane add and two lane-group swaps (v_permlane16_swap,
+// v_permlane32_swap).  T = 197: leaf 0 = keys 0..95 = tiles 0..5, leaf 1 = keys 96..191 (tiles
+// 6..11) + the tail 192..196 (tile 12: group 0's r = 0, 1, group 1's r = 0, 1, group 2's r = 0),
+// added in order in group 0's lanes and broadcast.  K rows are staged in LDS in this order.
+// P V: the contraction index kappa = 16 lg + 4 q + r of a 64-key chunk ch is (tile 4 ch + q, position
+// 4 lg + r), so lane (query, lg)'s B operand is its own P dwords of tiles 4 ch .. 4 ch + 3; V^T is
+// staged in LDS in that key order (64 B rows per (chunk, dim), 16-B chunks swizzled as k_pg's).
+// Every element goes through exactly k_attention<7, 197, true>'s operations (the same exps, sums,
+// P / context filters and exact fallbacks), so the context bytes are bit-identical to it
+// (tests/test_gpu_attention.py compares the two kernels).
+#ifndef NQK_ATTN16_QPF
+#define NQK_ATTN16_QPF 1
+#endif
+#ifndef NQK_ATTN16_MINB
+#define NQK_ATTN16_MINB 4  // workgroups (= waves per SIMD) per CU the register budget is sized for
+#endif
+constexpr int A16_T = 197, A16_NT = 13, A16_KP = 208, A16_VT = 4 * 64 * 64;
+__host__ __device__ constexpr int a16_sw(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }  // = pg_sw
+__device__ __forceinline__ int a16_key(int c, int p) { return 16 * c + 8 * ((p >> 1) & 1) + 2 * (p >> 2) + (p & 1); }
+__device__ __forceinline__ int xor16i(int x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];
+}
+__device__ __forceinline__ float xor16f(float x) { return __int_as_float(xor16i(__float_as_int(x))); }
+constexpr size_t attn16_lds() { return (size_t)A16_KP * 64 + A16_VT + (size_t)A16_KP * 4 + 64 * 4; }
+
+__global__ void __launch_bounds__(256, NQK_ATTN16_MINB)
+k_attn16(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int8_t* __restrict__ Vg,
+         int8_t* __restrict__ ctx, AttnArgs a) {
+  constexpr int T = A16_T, NT = A16_NT;
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  int8_t* const Ks = lds;                      // [208][64], chunk c of row R at c ^ a16_sw(R & 15)
+  int8_t* const Vt = Ks + A16_KP * 64;         // [4 chunks][64 dims][64 kappa]
+  int* const colK = reinterpret_cast<int*>(Vt + A16_VT);  // rowsum(K[n]) zq - zq zk 64, per position
+  int* const colV = colK + A16_KP;                         // colsum(V[:, d]) zp - zp zv T
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bh = blockIdx.x;
+  const int img = bh / a.H, head = bh - img * a.H;
+  const int8_t* q = Qg + (int64_t)bh * T * 64;
+  const int8_t* k = Kg + (int64_t)bh * T * 64;
+  const int8_t* v = Vg + (int64_t)bh * T * 64;
+  const int l15 = lane & 15, g = lane >> 4;
+
+  // ---- K rows in key order n(c, p), V^T in kappa order
+  for (int idx = tid; idx < A16_KP * 4; idx += 256) {
+    const int R = idx >> 2, ch = idx & 3;
+    const int n = a16_key(R >> 4, R & 15);
+    const v4i kv = n < T ? *reinterpret_cast<const v4i*>(k + n * 64 + ch * 16) : v4i{0, 0, 0, 0};
+    *reinterpret_cast<v4i*>(Ks + R * 64 + 16 * (ch ^ a16_sw(R & 15))) = kv;
+  }
+  {
+    // item tid = (chunk ch, tile-in-chunk qq, lane group lg, 16-dim block dm): keys k0, k0 + 1, k0 + 8,
+    // k0 + 9 (k0 = 16 (4 ch + qq) + 2 lg) = kappa 16 lg + 4 qq + 0..3 of chunk ch, 16 dims
+    const int ch = tid >> 6, qq = (tid >> 4) & 3, lg = (tid >> 2) & 3, dm = tid & 3;
+    const int k0 = 16 * (4 * ch + qq) + 2 * lg;
+    const int keys[4] = {k0, k0 + 1, k0 + 8, k0 + 9};
+    v4i w[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w[r] = keys[r] < T ? *reinterpret_cast<const v4i*>(v + keys[r] * 64 + dm * 16) : v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const uint32_t lo01 = __builtin_amdgcn_perm((uint32_t)w[1][gq], (uint32_t)w[0][gq], 0x05010400u);
+      const uint32_t hi01 = __builtin_amdgcn_perm((uint32_t)w[1][gq], (uint32_t)w[0][gq], 0x07030602u);
+      const uint32_t lo23 = __builtin_amdgcn_perm((uint32_t)w[3][gq], (uint32_t)w[2][gq], 0x05010400u);
+      const uint32_t hi23 = __builtin_amdgcn_perm((uint32_t)w[3][gq], (uint32_t)w[2][gq], 0x07030602u);
+      const uint32_t o[4] = {__builtin_amdgcn_perm(lo23, lo01, 0x05040100u), __builtin_amdgcn_perm(lo23, lo01, 0x07060302u),
+                             __builtin_amdgcn_perm(hi23, hi01, 0x05040100u), __builtin_amdgcn_perm(hi23, hi01, 0x07060302u)};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int d = 16 * dm + 4 * gq + kk;
+        *reinterpret_cast<uint32_t*>(Vt + (ch * 64 + d) * 64 + 16 * (lg ^ a16_sw(d & 15)) + 4 * qq) = o[kk];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < A16_KP) {
+    const int8_t* kr = Ks + tid * 64;  // (the chunk order does not matter for the sum)
+    colK[tid] = (sum16a(*reinterpret_cast<const v4i*>(kr)) + sum16a(*reinterpret_cast<const v4i*>(kr + 16)) +
+                 sum16a(*reinterpret_cast<const v4i*>(kr + 32)) + sum16a(*reinterpret_cast<const v4i*>(kr + 48))) * a.zq -
+                a.kq;
+  }
+  {
+    const int d = tid >> 2, ch = tid & 3;
+    const int8_t* vr = Vt + (ch * 64 + d) * 64;
+    int s = sum16a(*reinterpret_cast<const v4i*>(vr)) + sum16a(*reinterpret_cast<const v4i*>(vr + 16)) +
+            sum16a(*reinterpret_cast<const v4i*>(vr + 32)) + sum16a(*reinterpret_cast<const v4i*>(vr + 48));
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (ch == 0) colV[d] = s * a.zp - a.kp;
+  }
+  __syncthreads();
+
+  const int fo = l15 * 64 + 16 * (g ^ a16_sw(l15));  // fragment offset: row l15 of a 16-row block, chunk g
+  const float pqlo = a.lo_f - a.zp_p_f, pqhi = a.hi_f - a.zp_p_f, pmagic = 0x1.8p23f + a.zp_p_f;
+  auto q_frag = [&](int rt) __attribute__((always_inline)) {
+    const int mq = rt * 16 + l15;
+    return *reinterpret_cast<const v4i*>(q + (mq < T ? mq : T - 1) * 64 + g * 16);
+  };
+  v4i qnext = q_frag(wave);  // NQK_ATTN16_QPF: the next row tile's Q fragment loads under this one's work
+  for (int rt = wave; rt < NT; rt += 4) {
+    const int m = rt * 16 + l15;  // the lane's query row
+    const v4i qb = NQK_ATTN16_QPF ? qnext : q_frag(rt);
+    int nrowterm;
+    {
+      int rq = sum16a(qb);
+      rq += xor16i(rq);
+      rq += xor32i(rq);
+      nrowterm = -(rq * a.zk);
+      asm volatile("" : "+v"(nrowterm));
+    }
+    // ---- scores S^T tile by tile: e[c][r] = key n(c, 4 g + r) of the lane's query
+    float e[NT][4];
+    int imx = INT32_MIN, imn = INT32_MAX;
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      const v4i ck = *reinterpret_cast<const v4i*>(colK + 16 * c + 4 * g);
+      v4i acc = v4i{nrowterm - ck[0], nrowterm - ck[1], nrowterm - ck[2], nrowterm - ck[3]};
+      const v4i ka = *reinterpret_cast<const v4i*>(Ks + c * 1024 + fo);
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ka, qb, acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        v2f_t y = v2f_t{(float)acc[r], (float)acc[r + 1]} * v2f_t{a.s_qkd, a.s_qkd};
+        if (c == NT - 1) {  // the tile with pads (keys 197 .. 207): -inf, float max
+          const int n0 = 192 + 8 * (r >> 1) + 2 * g;
+          y = y + v2f_t{n0 < T ? 0.0f : -__builtin_inff(), n0 + 1 < T ? 0.0f : -__builtin_inff()};
+          mx = __builtin_fmaxf(mx, __builtin_fmaxf(y[0], y[1]));
+        } else {
+          imx = max(imx, max(acc[r], acc[r + 1]));
+          imn = min(imn, min(acc[r], acc[r + 1]));
+        }
+        e[c][r] = y[0];
+        e[c][r + 1] = y[1];
+      }
+    }
+    if (NQK_ATTN16_QPF && rt + 4 < NT) qnext = q_frag(rt + 4);
+    mx = __builtin_fmaxf(mx, (float)imx * a.s_qkd);
+    mx = __builtin_fmaxf(mx, xor16f(mx));
+    mx = __builtin_fmaxf(mx, xor32f(mx));
+    const float nm = -mx;
+    const float mn = (float)imn * a.s_qkd;
+    // every argument of tiles 0..11 in [-86.5, 0] in all lanes: NumPy's exp by np_expf_safe2;
+    // tile 12 (pads: -inf) and any other row by np_expf_nonpos2 (both equal NumPy's exp)
+    const bool esafe = __all(mn + nm >= NP_EXP_SAFE_LO);
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const v2f_t xa = v2f_t{e[c][r], e[c][r + 1]} + v2f_t{nm, nm};
+        const v2f_t x = (c < NT - 1 && esafe) ? np_expf_safe2(xa) : np_expf_nonpos2(xa);
+        e[c][r] = x[0];
+        e[c][r + 1] = x[1];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- NumPy's pairwise sum: leaf 0 = tiles 0..5, leaf 1 = tiles 6..11 + keys 192..196
+    float tot;
+    {
+      v2f_t a0 = v2f_t{e[0][0], e[0][1]}, a1 = v2f_t{e[6][0], e[6][1]};
+      a0 = a0 + v2f_t{e[0][2], e[0][3]};
+      a1 = a1 + v2f_t{e[6][2], e[6][3]};
+#pragma unroll
+      for (int c = 1; c < 6; ++c) {
+        a0 = a0 + v2f_t{e[c][0], e[c][1]};
+        a0 = a0 + v2f_t{e[c][2], e[c][3]};
+        a1 = a1 + v2f_t{e[c + 6][0], e[c + 6][1]};
+        a1 = a1 + v2f_t{e[c + 6][2], e[c + 6][3]};
+      }
+      float s0 = a0[0] + a0[1], s1 = a1[0] + a1[1];  // r_2g + r_2g+1
+      s0 = s0 + xor16f(s0);
+      s1 = s1 + xor16f(s1);
+      s0 = s0 + xor32f(s0);
+      s1 = s1 + xor32f(s1);
+      // the tail of leaf 1 in order (correct in lane group 0: 192, 193 its own, 194, 195 group 1's,
+      // 196 group 2's), then the total broadcast from group 0
+      const float x0 = e[NT - 1][0], x1 = e[NT - 1][1];
+      const float p0 = xor16f(x0), p1 = xor16f(x1), z0 = xor32f(x0);
+      s1 = ((((s1 + x0) + x1) + p0) + p1) + z0;
+      float t0 = s0 + s1;
+      const float t1 = xor16f(t0);
+      t0 = g == 1 ? t1 : t0;
+      const float t2 = xor32f(t0);
+      tot = g >= 2 ? t2 : t0;
+    }
+    const double rtot = 1.0 / (double)tot;
+    const float kpf = (float)(rtot * a.rs_p);
+    // ---- P = quantize(e / tot) (k_attention's two FAST forms and filters), 4 bytes per tile
+    const bool pq_nc = pqlo <= 0.0f && __all(kpf <= pqhi);
+    uint32_t dw[NT];
+    int rp = 0;
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      const v2f_t e0 = v2f_t{e[c][0], e[c][1]}, e1 = v2f_t{e[c][2], e[c][3]};
+      float worst;
+      uint32_t w;
+      if (pq_nc) {
+        const v2f_t k2 = v2f_t{kpf, kpf}, m2 = v2f_t{pmagic, pmagic};
+        const v2f_t s0 = __builtin_elementwise_fma(e0, k2, m2), s1 = __builtin_elementwise_fma(e1, k2, m2);
+        const v2f_t dd0 = __builtin_elementwise_fma(e0, k2, -(s0 - m2));
+        const v2f_t dd1 = __builtin_elementwise_fma(e1, k2, -(s1 - m2));
+        const v2f_t r0 = s0 - m2, r1 = s1 - m2;
+        worst = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(r0[0]), NQK_ATTN_PM_R, __builtin_fabsf(dd0[0])),
+                                                __builtin_fmaf(__builtin_fabsf(r0[1]), NQK_ATTN_PM_R, __builtin_fabsf(dd0[1]))),
+                                __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(r1[0]), NQK_ATTN_PM_R, __builtin_fabsf(dd1[0])),
+                                                __builtin_fmaf(__builtin_fabsf(r1[1]), NQK_ATTN_PM_R, __builtin_fabsf(dd1[1]))));
+        w = pack4_low(s0, s1);
+      } else {
+        v2f_t dd0, dd1;
+        const v2f_t tf0 = e0 * v2f_t{kpf, kpf}, tf1 = e1 * v2f_t{kpf, kpf};
+        const v2f_t s0 = round_magic2(tf0, pqlo, pqhi, pmagic, dd0);
+        const v2f_t s1 = round_magic2(tf1, pqlo, pqhi, pmagic, dd1);
+        worst = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(tf0[0]), NQK_ATTN_PM_T, __builtin_fabsf(dd0[0])),
+                                                __builtin_fmaf(__builtin_fabsf(tf0[1]), NQK_ATTN_PM_T, __builtin_fabsf(dd0[1]))),
+                                __builtin_fmaxf(__builtin_fmaf(__builtin_fabsf(tf1[0]), NQK_ATTN_PM_T, __builtin_fabsf(dd1[0])),
+                                                __builtin_fmaf(__builtin_fabsf(tf1[1]), NQK_ATTN_PM_T, __builtin_fabsf(dd1[1]))));
+        w = pack4_low(s0, s1);
+      }
+      if (c == NT - 1) {  // pad keys: P = 0
+        uint32_t keep = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) keep |= (192 + 8 * (r >> 1) + 2 * g + (r & 1) < T ? 0xffu : 0u) << (8 * r);
+        w &= keep;
+      }
+      if (__builtin_expect(__any(!(worst < 0x1.fffff8p-2f)), 0)) {
+        // the exact chain for the elements the filter could not decide (k_attention's fallbacks)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = 16 * c + 8 * (r >> 1) + 2 * g + (r & 1);
+          const float x = e[c][r];
+          bool slow;
+          if (pq_nc) {
+            const float rr = __builtin_fmaf(x, kpf, pmagic) - pmagic;
+            const float d = __builtin_fmaf(x, kpf, -rr);
+            slow = !(__builtin_fmaf(__builtin_fabsf(rr), NQK_ATTN_PM_R, __builtin_fabsf(d)) < 0x1.fffff8p-2f);
+          } else {
+            const float tf = x * kpf;
+            const float cf = __builtin_amdgcn_fmed3f(tf, pqlo, pqhi);
+            const float dv = __builtin_fabsf(cf - __builtin_rintf(cf));
+            slow = !(__builtin_fmaf(__builtin_fabsf(tf), NQK_ATTN_PM_T, dv) < 0x1.fffff8p-2f);
+          }
+          if (slow) {
+            const int qv = n < T ? quant_w(div_rc_w(x, rtot), a.s_p, a.rs_p, a.zp_p, a.lo, a.hi) : 0;
+            w = (w & ~(0xffu << (8 * r))) | ((uint32_t)(qv & 0xff) << (8 * r));
+          }
+        }
+      }
+      dw[c] = w;
+      rp = __builtin_amdgcn_sdot4((int)w, 0x01010101, rp, false);
+    }
+    rp += xor16i(rp);
+    rp += xor32i(rp);
+    // ---- context O^T = V^T P^T: chunk ch of 64 keys = this lane's P dwords of tiles 4 ch .. 4 ch + 3
+    v4i acc2[4];
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) acc2[mm] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch) {
+      const v4i pb = v4i{(int)dw[4 * ch], 4 * ch + 1 < NT ? (int)dw[4 * ch + 1] : 0, 4 * ch + 2 < NT ? (int)dw[4 * ch + 2] : 0,
+                         4 * ch + 3 < NT ? (int)dw[4 * ch + 3] : 0};
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        const v4i va = *reinterpret_cast<const v4i*>(Vt + (ch * 64 + 16 * mm) * 64 + fo);
+        acc2[mm] = __builtin_amdgcn_mfma_i32_16x16x64_i8(va, pb, acc2[mm], 0, 0, 0);
+      }
+    }
+    // ---- dequantize + quantize the context (k_attention's ctx_store): dims 16 mm + 4 g .. + 3
+    const int rowp = rp * a.zv;
+    int8_t* orow = ctx + ((int64_t)img * T + m) * a.ld_out + head * 64;
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      const int d0 = 16 * mm + 4 * g;
+      const v4i cv = *reinterpret_cast<const v4i*>(colV + d0);
+      float o[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) o[jj] = (float)(acc2[mm][jj] - rowp - cv[jj]) * a.s_pv;
+      v2f_t dd0, dd1;
+      const v2f_t t0 = v2f_t{o[0], o[1]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
+      const v2f_t t1 = v2f_t{o[2], o[3]} * v2f_t{a.rs_ctx_f, a.rs_ctx_f};
+      const v2f_t s0 = round_magic2(t0, a.lo_f - a.zp_ctx_f, a.hi_f - a.zp_ctx_f, 0x1.8p23f + a.zp_ctx_f, dd0);
+      const v2f_t s1 = round_magic2(t1, a.lo_f - a.zp_ctx_f, a.hi_f - a.zp_ctx_f, 0x1.8p23f + a.zp_ctx_f, dd1);
+      const float m0 = __builtin_fmaf(__builtin_fabsf(t0[0]), 0x1p-21f, __builtin_fabsf(dd0[0]));
+      const float m1 = __builtin_fmaf(__builtin_fabsf(t0[1]), 0x1p-21f, __builtin_fabsf(dd0[1]));
+      const float m2 = __builtin_fmaf(__builtin_fabsf(t1[0]), 0x1p-21f, __builtin_fabsf(dd1[0]));
+      const float m3 = __builtin_fmaf(__builtin_fabsf(t1[1]), 0x1p-21f, __builtin_fabsf(dd1[1]));
+      const uint32_t wm = __builtin_elementwise_max(__builtin_elementwise_max(__float_as_uint(m0), __float_as_uint(m1)),
+                                                    __builtin_elementwise_max(__float_as_uint(m2), __float_as_uint(m3)));
+      uint32_t packed = pack4_low(s0, s1);
+      if (__builtin_expect(__any(wm >= __float_as_uint(0x1.fffffcp-2f)), 0)) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int qv = quant_w(o[jj], a.s_ctx, a.rs_ctx, a.zp_ctx, a.lo, a.hi);
+          packed = (packed & ~(0xffu << (8 * jj))) | ((uint32_t)(qv & 0xff) << (8 * jj));
+        }
+      }
+      if (m < T) *reinterpret_cast<uint32_t*>(orow + d0) = packed;
+    }
+  }
+}
 }  // namespace
 }  // namespace nqk
 
@@ -1045,6 +1357,14 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   const size_t shm = (size_t)NT * 32 * 64 + (size_t)64 * a.PST + 256 + (size_t)(NT * 32 + 64) * 4;
   const dim3 grid((unsigned)batch_heads);
   const size_t shm_tail = shm + attn_tail_lds<7, 197, true>();
+  // round 6: the 16x16x64 four-lanes-per-row kernel for T = 197 FAST (NQK_ATTN16=0 keeps k_attention;
+  // on the bench's data 154 -> 143 us, profiles/r06_attn16.txt)
+  const char* a16v = getenv("NQK_ATTN16");
+  const bool a16 = a16v == nullptr || atoi(a16v) != 0;
+  if (T == 197 && fast && a16) {
+    hipLaunchKernelGGL(k_attn16, grid, dim3(256), attn16_lds(), stream(), q, k, v, ctx, a);
+    return launch_status("nqk_attention_fused(16)");
+  }
   switch (T == 197 ? (fast ? -1 : 0) : NT) {
 #define A(n) case n: hipLaunchKernelGGL((k_attention<n, 0, false>), grid, dim3(256), shm, stream(), q, k, v, ctx, a); break;
     case -1:  // ViT at 224 px (196 patches + CLS): the pairwise plan and pads fold at compile time

@@ -11,6 +11,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["k_attention", "k_attn16"])
+def attn_kernel(request, monkeypatch):
+    """Every case on both T = 197 kernels: round 6's k_attn16 (16x16x64, four lanes per query row,
+    NQK_ATTN16=1) and k_attention (other T take k_attention either way)."""
+    monkeypatch.setenv("NQK_ATTN16", "1" if request.param == "k_attn16" else "0")
+    return request.param
+
+
 def _run_both(B, H, T, zq, zk, zp, zv, zc, bw=8, seed=0, s_p=1.0 / 255, s_qk=(0.031, 0.027)):
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray
@@ -91,6 +99,18 @@ def test_attention_vit_base_batch():
     """ViT-Base shape at a larger batch (every (image, head) workgroup)."""
     f, u = _run_both(16, 12, 197, zq=-3, zk=4, zp=-128, zv=-1, zc=2, seed=7)
     np.testing.assert_array_equal(f, u)
+
+
+@pytest.mark.parametrize("s_p,zp,s_qk,zc", [(8.051e-05, -142, (0.02, 0.0225), -11), (1.0 / 255, -128, (0.031, 0.027), 2),
+                                            (3e-3, -120, (0.05, 0.06), 0)])
+def test_attn16_equals_k_attention(s_p, zp, s_qk, zc, monkeypatch):
+    """k_attn16 against k_attention directly (both FAST, T = 197), many workgroups, peaked and flat
+    softmaxes (the clamped and the clamp-free P paths), bit for bit."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("NQK_ATTN16", v)
+        outs.append(_run_both(24, 12, 197, zq=2, zk=-6, zp=zp, zv=-14, zc=zc, seed=abs(int(zp)) + 77, s_p=s_p, s_qk=s_qk)[0])
+    np.testing.assert_array_equal(outs[1], outs[0])
 
 
 def test_attention_rejects_unsupported_shapes():
