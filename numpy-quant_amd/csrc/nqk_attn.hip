@@ -18,6 +18,8 @@
 //                        writes of the transposed staging
 //   colK [NT*32], colV [64]   int32 zero-point column terms
 // 30 KiB per workgroup: three workgroups (12 waves) per CU; everything else is in VGPRs.
+#include <type_traits>
+
 #include "nqk_common.h"
 #include "nqk_numerics.h"
 
@@ -1128,6 +1130,9 @@ k_attn16(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int
     // every argument of tiles 0..11 in [-86.5, 0] in all lanes: NumPy's exp by np_expf_safe2;
     // tile 12 (pads: -inf) and any other row by np_expf_nonpos2 (both equal NumPy's exp)
     const bool esafe = __all(mn + nm >= NP_EXP_SAFE_LO);
+    // (tile by tile, pair by pair: a two-pair form with both chains interleaved in the source (s_nop
+    // 495 -> 70 in the kernel) and one branch hoisted over tiles 0..11 measured slower, 143 -> 165 us:
+    // profiles/r06_attn16.txt — at four waves per SIMD the other waves fill the hazard wait states)
 #pragma unroll
     for (int c = 0; c < NT; ++c) {
 #pragma unroll
