@@ -109,7 +109,7 @@ constexpr int pg_lds_bytes(int epi, bool b4, int wm = 1, int nk = 12) {
 #ifndef NQK_PG_DIAG
 #define NQK_PG_DIAG 0  // diagnostic builds only (tools/pg_diag.sh): 1 = no epilogue stores,
                        // 2 = trivial epilogue math, 4 = no operand loads, 8 = no barriers,
-                       // 16 = no fragment reads
+                       // 16 = no fragment reads, 4096 = no residual loads (zeros)
 #endif
 
 // physical 16-B chunk of logical chunk c in 64-B LDS row r is c ^ pg_sw(r): the 16 lanes of
@@ -817,7 +817,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     constexpr int i = decltype(I)::value;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      resv[i % 3][k] = pg_load16(s.tn * PG_BN + 64 * wn < N ? r_res : r_nul, res_off(s, i, k), 0u,
+      resv[i % 3][k] = pg_load16(s.tn * PG_BN + 64 * wn < N && (NQK_PG_DIAG & 4096) == 0 ? r_res : r_nul, res_off(s, i, k), 0u,
                                  NQK_PG_RLAUX >= 0 ? NQK_PG_RLAUX : (NK == 48 ? 2 : 0));
   };
   auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
