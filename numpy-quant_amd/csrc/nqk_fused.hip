@@ -694,7 +694,7 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
       // steps by DPP inside each 16-lane row: after step 1 the values are uniform per lane pair, after
       // step 2 per quad, after step 3 per leaf, so quad_perm [1,0,3,2], quad_perm [2,3,0,1],
       // row_half_mirror and row_mirror pair exactly the NumPy partners (xor 1, 2, 4, 8)
-      float xv[2][12], nmean[2], inv[2];
+      float xv[2][12];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const float* irow = lnimg + (8 * wave + 4 * h2 + jr) * LN_IMGS;
@@ -707,56 +707,54 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
         a = a + ln_dpp<0x141>(a);
         return a + ln_dpp<0x140>(a);
       };
+      // the two row groups' chains as one packed pair per lane (row 0 in .x, row 1 in .y): per lane the
+      // same IEEE operations in the same order as the scalar chains, one issue slot for both rows
+      v2f_t nm2, inv2;
       {
-        float s0 = xv[0][0], s1 = xv[1][0];
+        v2f_t sa = v2f_t{xv[0][0], xv[1][0]};
+#pragma unroll
+        for (int i = 1; i < 12; ++i) sa = sa + v2f_t{xv[0][i], xv[1][i]};
+        const float s0 = tree16(sa[0]), s1 = tree16(sa[1]);
+        nm2 = v2f_t{-(s0 / 192.0f), -(s1 / 192.0f)};
+        v2f_t d = v2f_t{xv[0][0], xv[1][0]} + nm2;
+        v2f_t va = d * d;
 #pragma unroll
         for (int i = 1; i < 12; ++i) {
-          s0 = s0 + xv[0][i];
-          s1 = s1 + xv[1][i];
+          d = v2f_t{xv[0][i], xv[1][i]} + nm2;
+          va = va + d * d;
         }
-        s0 = tree16(s0);
-        s1 = tree16(s1);
-        nmean[0] = -(s0 / 192.0f);
-        nmean[1] = -(s1 / 192.0f);
+        const float v0 = tree16(va[0]), v1 = tree16(va[1]);
+        inv2 = v2f_t{1.0f / __builtin_sqrtf(v0 / 192.0f + e.ln_eps), 1.0f / __builtin_sqrtf(v1 / 192.0f + e.ln_eps)};
       }
-      {
-        float v0, v1;
-        {
-          const float d0 = xv[0][0] + nmean[0], d1 = xv[1][0] + nmean[1];
-          v0 = d0 * d0;
-          v1 = d1 * d1;
-        }
+      // normalize + affine of 12 contiguous columns of both rows (inside one leaf: 96 = 8 x 12), pairs (row 0, row 1)
+      float yv[2][12];
 #pragma unroll
-        for (int i = 1; i < 12; ++i) {
-          const float d0 = xv[0][i] + nmean[0], d1 = xv[1][i] + nmean[1];
-          v0 = v0 + d0 * d0;
-          v1 = v1 + d1 * d1;
+      for (int k = 0; k < 3; ++k) {
+        const float4 a4 = *reinterpret_cast<const float4*>(lnimg + (8 * wave + jr) * LN_IMGS + ln_ipos(12 * c16) + 4 * k);
+        const float4 b4 = *reinterpret_cast<const float4*>(lnimg + (8 * wave + 4 + jr) * LN_IMGS + ln_ipos(12 * c16) + 4 * k);
+        const float xa[4] = {a4.x, a4.y, a4.z, a4.w}, xb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const v2f_t y2 = (((v2f_t{xa[q], xb[q]} + nm2) * inv2) * v2f_t{lg[4 * k + q], lg[4 * k + q]}) +
+                           v2f_t{lb[4 * k + q], lb[4 * k + q]};
+          yv[0][4 * k + q] = y2[0];
+          yv[1][4 * k + q] = y2[1];
         }
-        v0 = tree16(v0);
-        v1 = tree16(v1);
-        inv[0] = 1.0f / __builtin_sqrtf(v0 / 192.0f + e.ln_eps);
-        inv[1] = 1.0f / __builtin_sqrtf(v1 / 192.0f + e.ln_eps);
       }
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int rr = 8 * wave + 4 * h2 + jr;  // row of the pass
-        // normalize + affine + quantize 12 contiguous columns (inside one leaf: 96 = 8 x 12)
-        const float* src = lnimg + rr * LN_IMGS + ln_ipos(12 * c16);
         uint32_t pk[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const float4 x4 = *reinterpret_cast<const float4*>(src + 4 * k);
-          const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
-          float yv[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) yv[q] = (((xs[q] + nmean[h2]) * inv[h2]) * lg[4 * k + q]) + lb[4 * k + q];
+          const float y4[4] = {yv[h2][4 * k], yv[h2][4 * k + 1], yv[h2][4 * k + 2], yv[h2][4 * k + 3]};
           if (e.ln_mq) {
-            pk[k] = ln_quant4(yv, e.ln_rs, e.ln_q);
+            pk[k] = ln_quant4(y4, e.ln_rs, e.ln_q);
           } else {
             uint32_t w = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const float t = (float)((double)yv[q] * e.ln_rs);
+              const float t = (float)((double)y4[q] * e.ln_rs);
               const double uu = e.ln_zp + (double)t;
               const int qv = (int)__builtin_rint(__builtin_fmin(__builtin_fmax(uu, e.ln_lo), e.ln_hi));
               w |= ((uint32_t)(qv & 0xff)) << (8 * q);
