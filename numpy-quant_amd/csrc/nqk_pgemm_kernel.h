@@ -90,6 +90,9 @@ constexpr int pg_lds_bytes(int epi, bool b4, int wm = 1, int nk = 12) {
 #define NQK_PG_RLAUX -1  // cache-policy bits of the RESID epilogue's residual loads: -1 = nt for K = 3072
                          // (FFN-down 144 -> 138 us) and plain for K = 768 (nt: out-proj 59 -> 70 us)
 #endif
+#ifndef NQK_PG_RESQ
+#define NQK_PG_RESQ 3  // the residual epilogue's subtiles of residual rows in flight (round 6 A/B: 4)
+#endif
 #ifndef NQK_PG_SPREAD
 #define NQK_PG_SPREAD 0  // 1: the stage's LDS-DMA pieces spread over the first half step (A/B variant)
 #endif
@@ -809,7 +812,8 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   constexpr int TR_ROW = PG_TR_ROW;
   int8_t* const tr = lds + (B4 || WM == 2 ? COLP + 4096 : 2 * STG) + wave * (16 * TR_ROW);
   const int ta = lane & 15, tb = lane >> 4;
-  v4u resv[3][4];
+  constexpr int RQ = NQK_PG_RESQ;  // residual subtiles in flight (register slots)
+  v4u resv[RQ][4];
   auto res_off = [&](const Src& s, int i, int k) __attribute__((always_inline)) {
     return (uint32_t)(((s.r0 + PG_BM * wm + 16 * i + 4 * k + tb) * e.ldo + s.tn * PG_BN + 64 * wn + 4 * ta) * 4);
   };
@@ -817,7 +821,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     constexpr int i = decltype(I)::value;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      resv[i % 3][k] = pg_load16(s.tn * PG_BN + 64 * wn < N && (NQK_PG_DIAG & 4096) == 0 ? r_res : r_nul, res_off(s, i, k), 0u,
+      resv[i % RQ][k] = pg_load16(s.tn * PG_BN + 64 * wn < N && (NQK_PG_DIAG & 4096) == 0 ? r_res : r_nul, res_off(s, i, k), 0u,
                                  NQK_PG_RLAUX >= 0 ? NQK_PG_RLAUX : (NK == 48 ? 2 : 0));
   };
   auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
@@ -835,7 +839,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
       v4i t[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) t[k] = *reinterpret_cast<const v4i*>(tr + (4 * k + tb) * TR_ROW + 16 * ta);
-      const v4u(&rv)[4] = resv[i % 3];
+      const v4u(&rv)[4] = resv[i % RQ];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         v4u st;
@@ -855,7 +859,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
         else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, res_off(s, i, k), 0, NQK_PG_STAUX_RESID);
       }
-      if constexpr (i + 2 < 8) res_issue(s, ic<i + 2>{});
+      if constexpr (i + RQ - 1 < 8) res_issue(s, ic<i + RQ - 1>{});
     });
   };
 
@@ -1074,8 +1078,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     // stages (slots 0 and 1: last read before step NK - 2's barrier); a barrier frees slot 2
     // (stage NK - 1) for the epilogue's transposes
     if constexpr (RESID) {
-      res_issue(cur, ic<0>{});
-      res_issue(cur, ic<1>{});
+      sfor<0, RQ - 1>([&](auto R) __attribute__((always_inline)) { res_issue(cur, R); });
       if constexpr (!B4 && WM == 1) __builtin_amdgcn_s_barrier();  // (B4, WM = 2: the scratch is not in the ring)
     }
     // (the last tile re-stages its own first stages: never read, drained at the end; the
