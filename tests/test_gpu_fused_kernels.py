@@ -368,6 +368,16 @@ def test_persistent_projection_gemm_equals_big_tile(epi_name, M, N, K, bw, monke
 @pytest.mark.parametrize("M,K", [(128 * 197, 192), (128 * 197, 768), (1000, 192), (131, 768), (256 * 197, 768)])
 @pytest.mark.parametrize("bw,zp,f64q", [(8, -5, False), (8, 140, False), (4, 2, False), (8, 3, True)])
 def test_resid_epilogue_fused_layernorm_equals_ln_quant(M, K, bw, zp, f64q, monkeypatch):
+    _fused_ln_case(M, K, bw, zp, f64q, monkeypatch, wbits=8)
+
+
+@pytest.mark.parametrize("M,K", [(128 * 197, 192), (1000, 768)])
+def test_resid_epilogue_fused_layernorm_int4_weights(M, K, monkeypatch):
+    """The same with nibble-packed int4 weights (k_qgemm_big<RESID, B4, LN>)."""
+    _fused_ln_case(M, K, 4, 1, False, monkeypatch, wbits=4)
+
+
+def _fused_ln_case(M, K, bw, zp, f64q, monkeypatch, wbits):
     """Round 6: the residual GEMM's epilogue with the consumer LayerNorm fused
     (nqk_epilogue.ln_out, k_qgemm_big<RESID, LN>, N = 192: ViT-Ti's out-projection K = 192 and FFN-down
     K = 768) writes the same f32 rows as without it, and its int8 LayerNorm output equals nqk_ln_quant
@@ -382,7 +392,7 @@ def test_resid_epilogue_fused_layernorm_equals_ln_quant(M, K, bw, zp, f64q, monk
     N = 192
     rng = np.random.default_rng(M + K + bw + zp)
     a = DeviceArray.from_host(rng.integers(-128, 128, size=(M, K), dtype=np.int8))
-    bt_h = rng.integers(-30, 31, size=(N, K), dtype=np.int8)
+    bt_h = rng.integers(-30, 31, size=(N, K), dtype=np.int8) if wbits == 8 else rng.integers(-8, 8, size=(N, K), dtype=np.int8)
     bt = DeviceArray.from_host(bt_h)
     col_h = bt_h.astype(np.int64).sum(axis=1)
     col = DeviceArray.from_host(col_h)
@@ -391,7 +401,8 @@ def test_resid_epilogue_fused_layernorm_equals_ln_quant(M, K, bw, zp, f64q, monk
     g = DeviceArray.from_host((1 + 0.1 * rng.standard_normal(N)).astype(np.float32))
     b = DeviceArray.from_host((0.1 * rng.standard_normal(N)).astype(np.float32))
     eps, s_ln = float(np.float32(1e-12)), float(np.float32(0.021 if bw == 8 else 0.4))
-    bp = _pack_b(bt, 8)
+    bp = _pack_b(bt, wbits)
+    assert bp is not None and bp[1] == (2 if wbits == 4 else 1)
     outs = []
     for fuse in (False, True):
         e = _lib.Epilogue()
