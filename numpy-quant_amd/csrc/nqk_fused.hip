@@ -114,6 +114,7 @@ struct Epi {
   int ln_mq;                 // 1: the magic-number output quantize (exact, host-checked as nqk_ln_quant's)
   double ln_rs, ln_zp, ln_lo, ln_hi;
   LnQ ln_q;
+  int xcds;                  // XCDs of the device (xcd_tile's band count)
 };
 
 enum { EPI_QKV = 0, EPI_SCORES = 1, EPI_PV = 2, EPI_RESID = 3, EPI_GELU = 4, EPI_NULL = 5 };
@@ -418,9 +419,10 @@ k_qgemm_epi(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   // XCD-aware tile order: consecutive tiles that share an A row panel land on one XCD
   const int nwg = tiles_m * tiles_n;
   int wg = blockIdx.x;
-  if (nwg >= 8) {
-    const int q = nwg / 8, r = nwg % 8, x = wg % 8;
-    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
+  const int xc = e.xcds;
+  if (nwg >= xc && xc > 0) {
+    const int q = nwg / xc, r = nwg % xc, x = wg % xc;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / xc;
   }
   const int tm = wg / tiles_n, tn = wg % tiles_n;
   const int m0 = tm * FBM, n0 = tn * FBN;
@@ -788,7 +790,7 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
   }
 }
 
-// XCD-aware tile order: XCD x (= blockIdx % 8) walks one contiguous band of tiles, so
+// XCD-aware tile order: XCD x (= blockIdx % XCDs) walks one contiguous band of tiles, so
 // the blocks that share an A row panel share one L2
 #ifndef NQK_STAGGER
 #define NQK_STAGGER 0
@@ -799,11 +801,11 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
 #ifndef NQK_TILE_ORDER
 #define NQK_TILE_ORDER 0  // diagnostic builds: 1 = plain block order, 2 = column-panel bands
 #endif
-__device__ __forceinline__ int xcd_tile(int nwg) {
+__device__ __forceinline__ int xcd_tile(int nwg, int xc) {
   int wg = blockIdx.x;
-  if (NQK_TILE_ORDER != 1 && nwg >= 8) {
-    const int q = nwg / 8, r = nwg % 8, x = wg % 8;
-    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / 8;
+  if (NQK_TILE_ORDER != 1 && nwg >= xc && xc > 0) {
+    const int q = nwg / xc, r = nwg % xc, x = wg % xc;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + wg / xc;
   }
   return wg;
 }
@@ -841,7 +843,7 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
     for (int i = 0; i < NQK_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
   int tm, tn;
-  tile_of(xcd_tile(tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  tile_of(xcd_tile(tiles_m * tiles_n, e.xcds), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave;  // 4 waves along N
@@ -998,7 +1000,7 @@ k_qgemm_pp(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, i
   constexpr int STAGE = (BM + GBN) * GBK;  // 32 KiB
   extern __shared__ __attribute__((aligned(16))) int8_t lds[];
   int tm, tn;
-  tile_of(xcd_tile(tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  tile_of(xcd_tile(tiles_m * tiles_n, e.xcds), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * GBN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar branches
@@ -2289,6 +2291,16 @@ static Epi make_epi(const nqk_epilogue* p) {
   e.colterm = p->colterm;
   e.lof = (float)e.lo;
   e.hif = (float)e.hi;
+  e.xcds = [] {
+    static int n = 0;
+    if (n == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess ||
+          n <= 0)
+        n = 8;
+    }
+    return n;
+  }();
   e.ln_g = p->ln_gamma;
   e.ln_b = p->ln_beta;
   e.ln_out = p->ln_out;

@@ -233,7 +233,7 @@ struct EmbedEpi {
   const float* bias;
   const float* pos;  // [HW + 1][N]
   int64_t hw;
-  int xcd;  // k_embed_q: 1 = XCD-aware tile order (a row panel's column tiles on one XCD)
+  int xcd;  // k_embed_q: the XCD count for the XCD-aware tile order (a row panel's column tiles on one XCD), 0 = off
 };
 
 template <bool EMBED, bool AL16, bool VEC = false>
@@ -411,6 +411,18 @@ k_sgemm_mfma(const float* __restrict__ A, const float* __restrict__ B, float* __
 // A: the thread of row r (tid & 127) and half hf (tid >> 7, wave-uniform) keeps the 3 channel
 // rows (3 x 16 B) of its patch for the current kernel row ki (3 k-tiles) in registers and
 // writes its 8 k values of each k-tile as two ds_write_b128.
+// XCDs of the device (hipDeviceAttributeNumberOfXccs; 8 on MI355X): the round-robin unit of the
+// XCD-aware tile orders (not a constant)
+static int num_xcds() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess ||
+        n <= 0)
+      n = 8;
+  }
+  return n;
+}
 constexpr int EQ_ROW = 20;  // floats per LDS operand row (16 + 4 padding)
 #ifndef NQK_EMBED_PXD
 #define NQK_EMBED_PXD 1
@@ -433,7 +445,7 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
   int64_t tm = blockIdx.y, tn = blockIdx.x;
   if (ee.xcd) {
     const int64_t gx = gridDim.x, T = gx * gridDim.y, b = (int64_t)blockIdx.y * gx + blockIdx.x;
-    const int64_t x = b % 8, q8 = T / 8, r8 = T % 8;
+    const int64_t XC = ee.xcd, x = b % XC, q8 = T / XC, r8 = T % XC;
     const int64_t tile = x * q8 + (x < r8 ? x : r8) + b / 8;
     tm = tile / gx;
     tn = tile - tm * gx;
@@ -910,13 +922,13 @@ extern "C" int nqk_sgemm_embed(const float* cols, const float* w, const float* b
   const bool vec = (N % 4) == 0 && ((((uintptr_t)cols) | ((uintptr_t)w)) & 15) == 0 && !getenv("NQK_SGEMM_SCALAR");
   if (kblocks_al16(K, kb) && vec)
     hipLaunchKernelGGL((k_sgemm_mfma<true, true, true>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1,
-                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
+                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
   else if (kblocks_al16(K, kb))
     hipLaunchKernelGGL((k_sgemm_mfma<true, true>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1, N,
-                       (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
+                       (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
   else
     hipLaunchKernelGGL((k_sgemm_mfma<true, false>), g2, dim3(256), 0, stream(), cols, w, out, M, N, K, K, (int64_t)1,
-                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
+                       N, (int64_t)1, N, m, (int64_t)0, (int64_t)0, (int64_t)0, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
   if (int rc = launch_status("nqk_sgemm_embed")) return rc;
   hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);
   return launch_status("nqk_sgemm_embed(cls)");
@@ -943,10 +955,10 @@ extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float
   // profiles/r04_embed_1wg_streams_dropped.txt)
   if (N % 128 == 0) {
     hipLaunchKernelGGL(k_embed_q<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
-                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
+                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
   } else {
     hipLaunchKernelGGL(k_embed_q<1>, dim3((unsigned)(N / 64), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
-                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : 1});
+                       wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
   }
   if (int rc = launch_status("nqk_embed_q")) return rc;
   hipLaunchKernelGGL(k_embed_cls, dim3(grid_for(images * N)), dim3(kThreads), 0, stream(), cls, pos, out, images, hw, N);

@@ -83,6 +83,17 @@ static int pg_num_cus() {
   return n;
 }
 
+static int pg_num_xcds() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess ||
+        n <= 0)
+      n = 8;
+  }
+  return n;
+}
+
 // Launches k_pg for one projection GEMM when it takes the case; returns the kernel id for
 // nqk_qgemm_last_kernel (4 k_pg, 6 k_pg with the GELU table) if launched, 0 if the caller
 // must use another kernel, < 0 on error.  bp: the nqk_pack_pg image.  (Round 4's k_pg2 —
@@ -173,6 +184,7 @@ int pg_launch(int epi, const int8_t* a, const int8_t* bp, int64_t M, int64_t N, 
   e.add1 = p->add1;
   e.mul2 = p->mul2;
   e.ldo = (int)N;
+  e.xcds = pg_num_xcds();
   e.lut = glut ? p->gelu_lut : nullptr;
   e.lut_bytes = glut ? (uint32_t)((8 * p->lut_n + 15) & ~15) : 0u;
   e.gk = GLutK{p->lut_k[0], p->lut_k[1], p->lut_k[2], p->lut_k[3], p->lut_k[4]};

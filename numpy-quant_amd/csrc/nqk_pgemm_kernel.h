@@ -232,6 +232,7 @@ struct PgEpi {
   uint32_t lut_bytes;  // 8 * lut_n rounded up to 16: the table's buffer range
   GLutK gk;
   float blo, bhi;   // QKV: the clamp of v + 128 ([lo + 128, hi + 128] of the bit width)
+  int xcds;         // XCDs of the device (the band count of the XCD-aware tile order)
 };
 
 // quantize (numpy_quantization.py:24-34) with f64 zero-point add and clipping
@@ -417,7 +418,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   // tiles: the workgroups with blockIdx % 8 == x (one XCD under round-robin placement)
   // walk the band [lo, hi) of tile ids, every nx-th tile from lo + jx; tile ids are
   // row-panel major, so the tiles in flight on an XCD share A row panels in its L2.
-  const int G = gridDim.x, X = G < 8 ? G : 8, x = blockIdx.x % X;
+  const int G = gridDim.x, X = G < e.xcds ? G : e.xcds, x = blockIdx.x % X;
   const int nx = (G - x + X - 1) / X;
   const int lo = (int)((int64_t)ntiles * x / X), hi = (int)((int64_t)ntiles * (x + 1) / X);
   const int first = lo + (int)(blockIdx.x / X);
