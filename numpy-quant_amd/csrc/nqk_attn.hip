@@ -1012,7 +1012,11 @@ __device__ __forceinline__ int xor16i(int x) {
 __device__ __forceinline__ float xor16f(float x) { return __int_as_float(xor16i(__float_as_int(x))); }
 constexpr size_t attn16_lds() { return (size_t)A16_KP * 64 + A16_VT + (size_t)A16_KP * 4 + 64 * 4; }
 
-__global__ void __launch_bounds__(256, NQK_ATTN16_MINB)
+// NW: waves per workgroup, each taking row tiles wave, wave + NW, ... of the 13: 4 (ViT-Base: 3 072
+// (image, head) workgroups, 3 rounds of 4 per CU) or 5 (few (image, head) pairs, ViT-Ti: a
+// workgroup's life is ceil(13 / 5) = 3 row tiles instead of 4; round-6 A/B)
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, NQK_ATTN16_MINB)
 k_attn16(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int8_t* __restrict__ Vg,
          int8_t* __restrict__ ctx, AttnArgs a) {
   constexpr int T = A16_T, NT = A16_NT;
@@ -1030,13 +1034,13 @@ k_attn16(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int
   const int l15 = lane & 15, g = lane >> 4;
 
   // ---- K rows in key order n(c, p), V^T in kappa order
-  for (int idx = tid; idx < A16_KP * 4; idx += 256) {
+  for (int idx = tid; idx < A16_KP * 4; idx += 64 * NW) {
     const int R = idx >> 2, ch = idx & 3;
     const int n = a16_key(R >> 4, R & 15);
     const v4i kv = n < T ? *reinterpret_cast<const v4i*>(k + n * 64 + ch * 16) : v4i{0, 0, 0, 0};
     *reinterpret_cast<v4i*>(Ks + R * 64 + 16 * (ch ^ a16_sw(R & 15))) = kv;
   }
-  {
+  if (tid < 256) {  // (NW = 5: the fifth wave skips the V^T staging and the colV sums)
     // item tid = (chunk ch, tile-in-chunk qq, lane group lg, 16-dim block dm): keys k0, k0 + 1, k0 + 8,
     // k0 + 9 (k0 = 16 (4 ch + qq) + 2 lg) = kappa 16 lg + 4 qq + 0..3 of chunk ch, 16 dims
     const int ch = tid >> 6, qq = (tid >> 4) & 3, lg = (tid >> 2) & 3, dm = tid & 3;
@@ -1067,7 +1071,7 @@ k_attn16(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int
                  sum16a(*reinterpret_cast<const v4i*>(kr + 32)) + sum16a(*reinterpret_cast<const v4i*>(kr + 48))) * a.zq -
                 a.kq;
   }
-  {
+  if (tid < 256) {
     const int d = tid >> 2, ch = tid & 3;
     const int8_t* vr = Vt + (ch * 64 + d) * 64;
     int s = sum16a(*reinterpret_cast<const v4i*>(vr)) + sum16a(*reinterpret_cast<const v4i*>(vr + 16)) +
@@ -1085,7 +1089,7 @@ k_attn16(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int
     return *reinterpret_cast<const v4i*>(q + (mq < T ? mq : T - 1) * 64 + g * 16);
   };
   v4i qnext = q_frag(wave);  // NQK_ATTN16_QPF: the next row tile's Q fragment loads under this one's work
-  for (int rt = wave; rt < NT; rt += 4) {
+  for (int rt = wave; rt < NT; rt += NW) {
     const int m = rt * 16 + l15;  // the lane's query row
     const v4i qb = NQK_ATTN16_QPF ? qnext : q_frag(rt);
     int nrowterm;
@@ -1121,7 +1125,7 @@ k_attn16(const int8_t* __restrict__ Qg, const int8_t* __restrict__ Kg, const int
         e[c][r + 1] = y[1];
       }
     }
-    if (NQK_ATTN16_QPF && rt + 4 < NT) qnext = q_frag(rt + 4);
+    if (NQK_ATTN16_QPF && rt + NW < NT) qnext = q_frag(rt + NW);
     mx = __builtin_fmaxf(mx, (float)imx * a.s_qkd);
     mx = __builtin_fmaxf(mx, xor16f(mx));
     mx = __builtin_fmaxf(mx, xor32f(mx));
@@ -1367,7 +1371,13 @@ extern "C" int nqk_attention_fused(const int8_t* q, const int8_t* k, const int8_
   const char* a16v = getenv("NQK_ATTN16");
   const bool a16 = a16v == nullptr || atoi(a16v) != 0;
   if (T == 197 && fast && a16) {
-    hipLaunchKernelGGL(k_attn16, grid, dim3(256), attn16_lds(), stream(), q, k, v, ctx, a);
+    // NQK_ATTN16_NW=5: five waves per workgroup (A/B variant)
+    const char* nwv = getenv("NQK_ATTN16_NW");
+    const int nw = nwv ? atoi(nwv) : 4;
+    if (nw == 5)
+      hipLaunchKernelGGL(k_attn16<5>, grid, dim3(320), attn16_lds(), stream(), q, k, v, ctx, a);
+    else
+      hipLaunchKernelGGL(k_attn16<4>, grid, dim3(256), attn16_lds(), stream(), q, k, v, ctx, a);
     return launch_status("nqk_attention_fused(16)");
   }
   switch (T == 197 ? (fast ? -1 : 0) : NT) {

@@ -953,7 +953,9 @@ extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float
   // slower: 634 vs 625 us, profiles/r04_embed_ring_dropped.txt)
   // (also dropped: one workgroup per CU, 256 x 128 tiles, one wave per SIMD — 768 vs 605 us,
   // profiles/r04_embed_1wg_streams_dropped.txt)
-  if (N % 128 == 0) {
+  // (NQK_EMBED_WN1=1: the 128 x 64 tiles at N % 128 == 0 as well — 150 VGPRs, 3 workgroups per CU
+  // instead of 2, twice the tiles; round-6 A/B)
+  if (N % 128 == 0 && !getenv("NQK_EMBED_WN1")) {
     hipLaunchKernelGGL(k_embed_q<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
                        wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
   } else {

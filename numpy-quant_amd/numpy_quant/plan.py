@@ -503,7 +503,12 @@ class FusedEmbed:
                           self.wt.vp, self.bias.vp, self.cls.vp, self.posv.vp, ov.vp, nb, c, h, w, m.kh, m.kw,
                           self.kout)
 
-            streams.halves(n, part)
+            if os.environ.get("NQK_EMBED_WHOLE") and embed_q_fits(n, hw, self.kout):
+                # A/B variant (round 6): one whole-batch launch on stream 0; the next split step forks
+                streams.join()
+                part(0, 0, n)
+            else:
+                streams.halves(n, part)
             if t0 is not None:
                 KM.TIMER.end("embed_sgemm", t0, (2 * n * hw * self.kk * self.kout,
                                                  n * c * h * w + 4 * (self.kk * self.kout + n * (hw + 1) * self.kout)),

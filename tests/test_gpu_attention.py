@@ -11,11 +11,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["k_attention", "k_attn16"])
+@pytest.fixture(autouse=True, params=["k_attention", "k_attn16", "k_attn16_nw5"])
 def attn_kernel(request, monkeypatch):
     """Every case on both T = 197 kernels: round 6's k_attn16 (16x16x64, four lanes per query row,
-    NQK_ATTN16=1) and k_attention (other T take k_attention either way)."""
-    monkeypatch.setenv("NQK_ATTN16", "1" if request.param == "k_attn16" else "0")
+    NQK_ATTN16=1; four or five waves per workgroup, NQK_ATTN16_NW) and k_attention (other T take
+    k_attention either way)."""
+    monkeypatch.setenv("NQK_ATTN16", "0" if request.param == "k_attention" else "1")
+    monkeypatch.setenv("NQK_ATTN16_NW", "5" if request.param == "k_attn16_nw5" else "4")
     return request.param
 
 
