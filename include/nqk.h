@@ -154,15 +154,23 @@ int nqk_sgemm(const float* a, const float* b, float* c, int64_t batch, int64_t M
  * that to OpenBLAS's GEMV-T (vector_matrix -> cblas_sgemv), and this reproduces its order
  * bit for bit — the N columns split over `threads` chunks as OpenBLAS's gemv threading does
  * (one chunk when K*N < 460800), 8-lane fma / 4-lane SSE kernels per column class, K blocks
- * of 4096, trailing rows (oracle/openblas_order.py).  `threads` = OpenBLAS's thread count
- * of the NumPy being matched. */
+ * of 4096, trailing rows (oracle/openblas_order.py); for K <= 8 with ldb == K, OpenBLAS's
+ * small-m kernels in every chunk of at most 16 384 columns (their column classes identified
+ * in round 6: k_sgemv_small).  `threads` = OpenBLAS's thread count of the NumPy being matched. */
 int nqk_sgemv_t(const float* x, const float* bt, float* y, int64_t N, int64_t K, int64_t ldb, int64_t threads);
 
-/* The other one-row products of NumPy's matmul (model.py:122-131 Gemm / tensor.py:100-101
- * FTensor.matmul on one row): N == 1 (cblas_sdot: f32 products summed in double, restated
- * for K < 32) and K in 2..8 except 4 (OpenBLAS's small-m GEMV-T kernels: fma chains on
- * column blocks, multiply-add chains on leftover columns; see k_sgemv_small for the parts
- * not restated).  Same operand layout as nqk_sgemv_t; for N == 1 bt is the K-vector. */
+/* One-row float product y[N] = x[1][K] . B[K][N] with B row-major (b[K][ldb], ldb >= N: a MatMul's
+ * weight, tensor.py:100-101 FTensor.matmul -> np.matmul): NumPy hands it to OpenBLAS's GEMV-N, and
+ * this reproduces its order bit for bit (round 6, oracle/openblas_order.py sgemv_n: K <= 48 fma
+ * chains; N < 4 pairs; else the outputs split over `threads` chunks, blocks of 4096 outputs, the
+ * 8-row and 16-row kernels' groups of 8 products, trailing outputs as fma chains).  `threads` as
+ * nqk_sgemv_t. */
+int nqk_sgemv_n(const float* x, const float* b, float* y, int64_t N, int64_t K, int64_t ldb, int64_t threads);
+
+/* A 1 x 1 one-row product of NumPy's matmul (model.py:122-131 Gemm / tensor.py:100-101
+ * FTensor.matmul): cblas_sdot's order at every length (the SkylakeX vector kernel's
+ * accumulators over the first K & -32 products, the tail's f32 products summed in double;
+ * round 6).  N must be 1 (one-row products with N > 1: nqk_sgemv_t); bt is the K-vector. */
 int nqk_sgemv_small(const float* x, const float* bt, float* y, int64_t N, int64_t K, int64_t ldb);
 
 /* im2col for Conv (numpy_helper.py:18-70): x NCHW f32 -> cols[N*Ho*Wo][KH*KW*C]

@@ -733,9 +733,6 @@ k_sgemv_t(const float* __restrict__ x, const float* __restrict__ bt, float* __re
     } else if (cls == 1) {  // lanes 0-3: rows r = l mod 4, multiply then add
       if (l < 4)
         for (; i < nb; i += 4) acc = acc + xb[i + l] * a[i + l];
-    } else if (K == 4) {  // K = 4: the single leftover column is one multiply-add chain
-      if (l == 0)         // (identified against np.matmul: tests/test_host.py)
-        for (; i < nb; ++i) acc = acc + xb[i] * a[i];
     } else {  // lane l: set l / 4, row l % 4 of each 8-row step (prologue rows to set 0)
       if (nb & 4) {
         if (l < 4) acc = acc + xb[l] * a[l];
@@ -767,49 +764,208 @@ k_sgemv_t(const float* __restrict__ x, const float* __restrict__ bt, float* __re
   if (live && l == 0) y[j] = yv;
 }
 
-// One-row products OpenBLAS does not send through the GEMV-T kernels above (identified
-// against np.matmul, oracle/openblas_order.py sgemv_small / sdot, pinned by
-// tests/test_host.py):
-//  * N == 1 (NumPy's matmul takes cblas_sdot for a 1 x 1 result): below 32 rows the
-//    f32 products are summed in double, in order, and the sum rounded once to f32;
-//  * K in 2..8 except 4 (the AVX-512 small-m GEMV-T kernels): columns in blocks of 16
-//    (K = 2), 4 (K = 5) or 8 (K = 3, 6, 7) are k-ordered fma chains; the columns left over
-//    are multiply-add chains, except a leftover 4-column block for K = 3, 6, 7 and a last
-//    odd column for K = 3 (orders not restated: computed as fma chains; the host reports
-//    them, kernels.one_row_restated) and K = 8 (not restated at all).
+// One-row products outside the GEMV-T kernel above (round 6: every class identified against
+// np.matmul, oracle/openblas_order.py sdot / small_modes, pinned by tests/test_host.py):
+//  * N == 1 (NumPy's matmul takes cblas_sdot for a 1 x 1 result): the first n & -32 products by
+//    the SkylakeX vector kernel — lane l of the wave is element l of its four 16-wide fma
+//    accumulators over 64-element steps; folded to four 8-wide ones (low + high half), which
+//    continue over 32-element steps; ((a0 + a1) + a2) + a3, low + high 4, two horizontal adds —
+//    then the tail's f32 products added in double, the sum rounded once;
+//  * K <= 8 (OpenBLAS's small-m GEMV-T kernels, per thread chunk of at most 16 384 columns;
+//    wider chunks take the regular kernel's order, restated here for K <= 8): the column's
+//    class by its place in its chunk (small_modes), one lane per column.
+__device__ __forceinline__ void gemv_chunk(int64_t j, int64_t N, int threads, int64_t& j0, int64_t& w) {
+  int64_t rem = N;
+  j0 = 0;
+  for (int t = 0; rem > 0; ++t) {
+    int64_t c = threads - t > 0 ? (rem + threads - t - 1) / (threads - t) : rem;
+    c = c < 4 ? 4 : c;
+    c = c > rem ? rem : c;
+    if (j < j0 + c) {
+      w = c;
+      return;
+    }
+    j0 += c;
+    rem -= c;
+  }
+  w = rem;
+}
+
 __global__ void __launch_bounds__(256)
 k_sgemv_small(const float* __restrict__ x, const float* __restrict__ bt, float* __restrict__ y, int64_t N, int64_t K,
-              int64_t ldb) {
+              int64_t ldb, int threads) {
+  if (N == 1) {  // cblas_sdot: one wave
+    if (threadIdx.x >= 64) return;
+    const int l = threadIdx.x;
+    const float* w = bt;
+    const int64_t n1 = K & ~(int64_t)31, n64 = K & ~(int64_t)63;
+    float a = 0.0f;  // lane l: element l % 16 of 16-wide accumulator l / 16
+    int64_t i = 0;
+    for (; i < n64; i += 64) a = __builtin_fmaf(x[i + l], w[i + l], a);
+    // fold to 8 wide: accumulator q = l / 8 (lanes 0..31), element e = l % 8
+    const int q = (l >> 3) & 3, e = l & 7;
+    float a8 = __shfl(a, 16 * q + e, 64) + __shfl(a, 16 * q + 8 + e, 64);
+    if (l < 32)
+      for (int64_t k = i; k < n1; k += 32) a8 = __builtin_fmaf(x[k + l], w[k + l], a8);
+    // ((a0 + a1) + a2) + a3 per element e (lanes e, e + 8, e + 16, e + 24)
+    const float s8 = ((__shfl(a8, e, 64) + __shfl(a8, 8 + e, 64)) + __shfl(a8, 16 + e, 64)) + __shfl(a8, 24 + e, 64);
+    const float h = __shfl(s8, e & 3, 64) + __shfl(s8, (e & 3) + 4, 64);  // low + high 4
+    const float h01 = __shfl(h, 0, 64) + __shfl(h, 1, 64), h23 = __shfl(h, 2, 64) + __shfl(h, 3, 64);
+    if (l == 0) {
+      double d = n1 ? (double)(h01 + h23) : 0.0;
+      for (int64_t k = n1; k < K; ++k) {
+        const float p = x[k] * w[k];  // -ffp-contract=off: the f32 product, then the double add
+        d += (double)p;
+      }
+      y[0] = (float)d;
+    }
+    return;
+  }
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= N) return;
   const float* w = bt + j * ldb;
-  if (N == 1) {
-    double d = 0.0;
-    for (int64_t k = 0; k < K; ++k) {
-      const float p = x[k] * w[k];  // -ffp-contract=off: the f32 product, then the double add
-      d += (double)p;
+  float p[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = k < K ? x[k] * w[k] : 0.0f;
+  auto F = [&](int k, float acc) { return __builtin_fmaf(x[k], w[k], acc); };
+  int64_t j0, cw;
+  gemv_chunk(j, N, threads, j0, cw);
+  float r;
+  if (cw > 16384) {  // the regular kernel (k_sgemv_t's order) at K <= 8
+    const int m3 = (int)(K & 3);
+    float yv = 0.0f;
+    if (K == 8) yv = yv + (((p[0] + p[4]) + (p[1] + p[5])) + ((p[2] + p[6]) + (p[3] + p[7])));
+    else if (K >= 4) yv = yv + ((p[0] + p[1]) + (p[2] + p[3]));
+    const int k0 = K >= 4 ? 4 : 0;
+    if (m3 == 1) {
+      yv = __builtin_fmaf(w[k0], x[k0], yv);
+    } else if (m3 > 1) {
+      float t = __builtin_fmaf(w[k0], x[k0], w[k0 + 1] * x[k0 + 1]);
+      if (m3 == 3) t = __builtin_fmaf(w[k0 + 2], x[k0 + 2], t);
+      yv = yv + t;
     }
-    y[0] = (float)d;
+    r = yv;
+  } else {
+    // the small-m kernel's class of local column loc in a chunk of cw (oracle small_modes)
+    const int64_t loc = j - j0;
+    char c = 'M';
+    if (K == 4) {
+      c = loc < (cw & ~(int64_t)1) ? 'P' : 'M';
+    } else if (K == 8) {
+      const int64_t n4 = cw & ~(int64_t)3;
+      c = loc < n4 ? 'c' : ((cw & 2) && loc < n4 + 2 ? 'a' : 'e');
+    } else if (K == 1) {
+      c = 'F';
+    } else {
+      const int64_t blk = K == 2 ? 16 : (K == 5 ? 4 : 8);
+      const int64_t f_end = cw / blk * blk;
+      int64_t rr = cw - f_end, lo = loc - f_end;
+      if (loc < f_end) {
+        c = 'F';
+      } else {
+        if ((K == 3 || K == 6 || K == 7) && rr >= 4) {
+          if (lo < 4) c = 'b';
+          rr -= 4;
+          lo -= 4;
+        }
+        if (c != 'b' && K == 3) c = ((rr & 2) && lo < 2) ? 'M' : 'b';
+      }
+    }
+    switch (c) {
+      case 'F': {
+        float acc = 0.0f;
+        for (int k = 0; k < K; ++k) acc = F(k, acc);
+        r = acc;
+        break;
+      }
+      case 'P': r = (p[0] + p[1]) + (p[2] + p[3]); break;
+      case 'b':
+        if (K == 3) r = F(2, F(0, p[1]));
+        else if (K == 6) r = (p[0] + F(1, p[2])) + (p[3] + F(4, p[5]));
+        else r = (F(0, p[1]) + F(4, p[5])) + (F(2, p[3]) + p[6]);
+        break;
+      case 'c': r = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7])); break;
+      case 'a': r = ((p[0] + p[1]) + (p[4] + p[5])) + ((p[2] + p[3]) + (p[6] + p[7])); break;
+      case 'e': r = (((p[0] + p[4]) + (p[1] + p[5])) + (p[2] + p[6])) + (p[3] + p[7]); break;
+      default: {
+        float acc = 0.0f;
+        for (int k = 0; k < K; ++k) acc = acc + p[k];
+        r = acc;
+      }
+    }
+  }
+  y[j] = r;
+}
+
+// One-row product y[N] = x[1][K] . B[K][N] with B row-major (ldb >= N): NumPy's matmul hands it to
+// OpenBLAS's GEMV-N (vector_matrix -> cblas_sgemv on the row-major matrix; round 6: the order
+// identified against np.matmul, oracle/openblas_order.py sgemv_n, pinned by tests/test_host.py):
+//  * K <= 48: a k-ordered fma chain per output;
+//  * N < 4: pairs — t = t + fma(x_k, b_k, RN(x_{k+1} b_{k+1})) over k = 0, 2, .. below K & -4, then
+//    an fma chain over the rest;
+//  * else the outputs split over `threads` chunks (gemv_thread.c, as GEMV-T's columns); per chunk of
+//    w outputs, the last w & 3 are fma chains; the others go in blocks of 4 096 (the last block
+//    (w & 4095) - (w & 3)), and in a block of NB the first NB % 16 outputs take the 8- / 4-row
+//    kernel (groups of 8 products as two fma chains, even and odd, summed: y += a + b; a 4-group
+//    the same; 2- and 1-groups one chain), the rest the 16-row kernel (groups of 8, 4, 2, 1
+//    products as one fma chain each: y += chain).
+// One lane per output, K products serially (column j of B: adjacent lanes read adjacent floats).
+__global__ void __launch_bounds__(256)
+k_sgemv_n(const float* __restrict__ x, const float* __restrict__ b, float* __restrict__ y, int64_t N, int64_t K,
+          int64_t ldb, int threads) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  const float* c = b + j;
+  auto prod = [&](int64_t k, float acc) { return __builtin_fmaf(x[k], c[k * ldb], acc); };
+  auto chain = [&](int64_t k0, int64_t k1) {
+    float acc = 0.0f;
+    for (int64_t k = k0; k < k1; ++k) acc = prod(k, acc);
+    return acc;
+  };
+  if (K <= 48) {
+    y[j] = chain(0, K);
     return;
   }
-  const int64_t blk = K == 2 ? 16 : (K == 5 ? 4 : 8);
-  const int64_t f_end = N / blk * blk;
-  bool chain_fma = j < f_end || K == 8;
-  if (!chain_fma && (K == 3 || K == 6 || K == 7)) {
-    int64_t r = N - f_end, loc = j - f_end;
-    if (r >= 4) {
-      if (loc < 4) chain_fma = true;  // the 4-column block (not restated)
-      r -= 4;
-      loc -= 4;
-    }
-    if (!chain_fma && K == 3 && !((r & 2) && loc < 2)) chain_fma = true;  // K = 3: last odd column
+  if (N < 4) {
+    float t = 0.0f;
+    int64_t k = 0;
+    for (; k < (K & ~(int64_t)3); k += 2) t = t + prod(k, x[k + 1] * c[(k + 1) * ldb]);
+    for (; k < K; ++k) t = prod(k, t);
+    y[j] = t;
+    return;
   }
-  float acc = 0.0f;
-  if (chain_fma)
-    for (int64_t k = 0; k < K; ++k) acc = __builtin_fmaf(x[k], w[k], acc);
-  else
-    for (int64_t k = 0; k < K; ++k) acc = acc + x[k] * w[k];
-  y[j] = acc;
+  int64_t j0, w;
+  gemv_chunk(j, N, threads, j0, w);
+  const int64_t loc = j - j0, m3 = w & 3;
+  if (loc >= w - m3) {
+    y[j] = chain(0, K);
+    return;
+  }
+  const int64_t nfull = (w & ~(int64_t)3) / 4096, bi = loc / 4096;
+  const int64_t nb = bi < nfull ? 4096 : (w & 4095) - m3;
+  const bool two = (loc - bi * 4096) < nb % 16;  // the 8- / 4-row kernel
+  auto two_acc = [&](int64_t k0, int64_t size) {
+    float a = 0.0f, e = 0.0f;
+    for (int64_t q = 0; q < size; ++q) {
+      if (q & 1) e = prod(k0 + q, e);
+      else a = prod(k0 + q, a);
+    }
+    return a + e;
+  };
+  float yv = 0.0f;
+  const int64_t k8 = K & ~(int64_t)7;
+  for (int64_t g = 0; g < k8; g += 8) yv = yv + (two ? two_acc(g, 8) : chain(g, g + 8));
+  int64_t k = k8;
+  if (K & 4) {
+    yv = yv + (two ? two_acc(k, 4) : chain(k, k + 4));
+    k += 4;
+  }
+  if (K & 2) {
+    yv = yv + chain(k, k + 2);
+    k += 2;
+  }
+  if (K & 1) yv = yv + chain(k, k + 1);
+  y[j] = yv;
 }
 
 }  // namespace
@@ -1000,16 +1156,31 @@ extern "C" int nqk_sgemv_t(const float* x, const float* bt, float* y, int64_t N,
   if (threads < 1 || threads > 1024) return fail("nqk_sgemv_t: 1 <= threads <= 1024 expected");
   // interface/gemv.c: one thread below m * n = 115200 * GEMM_MULTITHREAD_THRESHOLD (4)
   const int t = (K * N < 115200 * 4) ? 1 : (int)threads;
+  if (K <= 8 && ldb == K && N > 1) {  // the small-m kernels (chunks <= 16 384 columns) and K <= 8 of the regular one
+    hipLaunchKernelGGL(k_sgemv_small, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream(), x, bt, y, N, K, ldb, t);
+    return launch_status("nqk_sgemv_t(small)");
+  }
   const int64_t lanes = N * 8;
   hipLaunchKernelGGL(k_sgemv_t, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream(), x, bt, y, N, K, ldb, t);
   return launch_status("nqk_sgemv_t");
+}
+
+extern "C" int nqk_sgemv_n(const float* x, const float* b, float* y, int64_t N, int64_t K, int64_t ldb,
+                           int64_t threads) {
+  if (N <= 0) return 0;
+  if (K <= 0) return fail("nqk_sgemv_n: K >= 1 expected");
+  if (ldb < N) return fail("nqk_sgemv_n: ldb < N");
+  if (threads < 1 || threads > 1024) return fail("nqk_sgemv_n: 1 <= threads <= 1024 expected");
+  const int t = (K * N < 115200 * 4) ? 1 : (int)threads;  // interface/gemv.c, as nqk_sgemv_t
+  hipLaunchKernelGGL(k_sgemv_n, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream(), x, b, y, N, K, ldb, t);
+  return launch_status("nqk_sgemv_n");
 }
 
 extern "C" int nqk_sgemv_small(const float* x, const float* bt, float* y, int64_t N, int64_t K, int64_t ldb) {
   if (N <= 0) return 0;
   if (K <= 0) return fail("nqk_sgemv_small: K >= 1 expected");
   if (ldb < K) return fail("nqk_sgemv_small: ldb < K");
-  if (N > 1 && !(K >= 2 && K <= 8 && K != 4)) return fail("nqk_sgemv_small: N == 1, or K in 2..8 except 4 expected");
-  hipLaunchKernelGGL(k_sgemv_small, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream(), x, bt, y, N, K, ldb);
+  if (N != 1) return fail("nqk_sgemv_small: N == 1 (cblas_sdot) expected; one-row products with N > 1 are nqk_sgemv_t's");
+  hipLaunchKernelGGL(k_sgemv_small, dim3(1), dim3(64), 0, stream(), x, bt, y, N, K, ldb, 1);
   return launch_status("nqk_sgemv_small");
 }

@@ -87,6 +87,7 @@ SIGNATURES = {
     "nqk_sgemm": [_p, _p, _p, _l, _l, _l, _l, _l, _l, _l, _l, _l, _lp, _l, _l, _l],
     "nqk_sgemv_t": [_p, _p, _p, _l, _l, _l, _l],
     "nqk_sgemv_small": [_p, _p, _p, _l, _l, _l],
+    "nqk_sgemv_n": [_p, _p, _p, _l, _l, _l, _l],
     "nqk_im2col": [_p, _p] + [_l] * 12,
     "nqk_binary_f32": [_i, _p, _p, _p, _i, _lp, _lp, _lp],
     "nqk_unary_f32": [_i, _p, _p, _l],

@@ -335,40 +335,27 @@ def openblas_threads() -> int:
 
 def gemv_t_applies(M: int, N: int, K: int) -> bool:
     """NumPy sends a one-row product x[1, K] @ B[K, N] (N > 1) whose B has unit stride
-    along K to OpenBLAS GEMV-T; nqk_sgemv_t reproduces its order for K >= 9 and K = 1, 4
-    (pinned against np.matmul; K in 2..8 other than 4 take OpenBLAS's small-m kernels:
-    small_one_row / nqk_sgemv_small)."""
-    return M == 1 and N > 1 and (K >= 9 or K in (1, 4))
+    along K to OpenBLAS GEMV-T; nqk_sgemv_t reproduces its order for every K (the regular
+    kernels, and for K <= 8 the small-m kernels of each thread chunk of at most 16 384
+    columns: oracle/openblas_order.py, pinned against np.matmul)."""
+    return M == 1 and N > 1
 
 
 def small_one_row(N: int, K: int) -> bool:
-    """One-row products NumPy does not send to the GEMV-T kernels that nqk_sgemv_t restates:
-    a 1 x 1 result (cblas_sdot) and K in 2..8 except 4 (OpenBLAS's small-m GEMV-T kernels);
-    nqk_sgemv_small computes them."""
-    return N == 1 or (2 <= K <= 8 and K != 4)
+    """A one-row product with a 1 x 1 result: NumPy calls cblas_sdot (nqk_sgemv_small)."""
+    return N == 1
 
 
 def one_row_restated(N: int, K: int) -> bool:
     """Whether x[1, K] @ B[K, N] with B's columns contiguous (a Gemm's w.T) is computed in
-    NumPy's exact order (pinned against np.matmul, tests/test_host.py): sdot below 32 rows;
-    GEMV-T for K = 1, 4 and K >= 9; the small-m kernels for K = 2, 5 (every N), K = 6, 7
-    when N % 8 < 4 and K = 3 when N % 8 in (0, 2).  Elsewhere (sdot from 32 rows, the
-    4-column blocks of K = 3, 6, 7, K = 8) the result may differ by ulps."""
-    if N == 1:
-        return K < 32
-    if K in (2, 5):
-        return True
-    if K in (6, 7):
-        return N % 8 < 4
-    if K == 3:
-        return N % 8 in (0, 2)
-    if K == 8:
-        return False
-    return gemv_t_applies(1, N, K)
+    NumPy's exact order (pinned against np.matmul, tests/test_host.py): since round 6 every
+    such product is — sdot at every length, GEMV-T's regular and small-m kernels at every K.
+    (A one-row product against a row-major B — a MatMul's weight — is GEMV-N: nqk_sgemv_n.)"""
+    return N >= 1 and K >= 1
 
 
 def sgemv_small(x: DeviceArray, bt: DeviceArray) -> DeviceArray:
-    """y[1, N] = x[1, K] . bt[N, K]^T for small_one_row shapes (nqk_sgemv_small)."""
+    """y[1, 1] = x[1, K] . bt[1, K]^T in cblas_sdot's order (nqk_sgemv_small)."""
     N, Kb = bt.shape
     K = x.shape[-1]
     if Kb != K or x.size != K:
@@ -395,9 +382,8 @@ def matmul_f32(a: DeviceArray, b: DeviceArray) -> DeviceArray:
     K2, N = b.shape[-2:]
     if K != K2:
         raise ValueError(f"matmul: mismatch in core dimension ({K} vs {K2})")
-    if a.ndim == 2 and b.ndim == 2 and M == 1 and N == 1:
-        # a 1 x 1 result: NumPy's matmul calls cblas_sdot (nqk_sgemv_small)
-        return sgemv_small(a, b.reshape((1, K)))
+    if (M == 1 or N == 1) and K > 1:
+        return _matmul_level2(a, b, M, N, K)
     out_batch, bmap = batch_map(a.shape[:-2], b.shape[:-2])
     if bmap is None:
         a = materialize_broadcast(a, out_batch + (M, K))
@@ -406,6 +392,41 @@ def matmul_f32(a: DeviceArray, b: DeviceArray) -> DeviceArray:
     nb = int(math.prod(out_batch))
     c = sgemm(a, K, 1, b, N, 1, M, N, K, batch=nb, bmap=bmap, a_ms=M * K, b_ms=K * N)
     return c.reshape(out_batch + (M, N))
+
+
+def _matmul_level2(a: DeviceArray, b: DeviceArray, M: int, N: int, K: int) -> DeviceArray:
+    """np.matmul where one side of each product is a vector: NumPy's matmul (matmul.cpp special
+    cases, per matrix of a stack) calls cblas_sdot for a 1 x 1 result, and cblas_sgemv for
+    vector @ matrix — OpenBLAS GEMV-N on a row-major matrix (nqk_sgemv_n) — and for matrix @
+    vector — GEMV-T over the matrix's rows (nqk_sgemv_t); each restated bit for bit
+    (oracle/openblas_order.py, round 6).  (K = 1 stays on the GEMM path: NumPy's own loop, one
+    product per output.)"""
+    out_batch = tuple(np.broadcast_shapes(a.shape[:-2], b.shape[:-2]))
+    if a.shape[:-2] != out_batch:
+        a = materialize_broadcast(a, out_batch + (M, K))
+    if b.shape[:-2] != out_batch:
+        b = materialize_broadcast(b, out_batch + (K, N))
+    c = DeviceArray(out_batch + (M, N), np.float32)
+    t = openblas_threads()
+    for i in range(int(math.prod(out_batch))):
+        ai, bi, ci = a.offset_view(i * M * K, (M, K)), b.offset_view(i * K * N, (K, N)), c.offset_view(i * M * N, (M, N))
+        if M == 1 and N == 1:
+            _lib.call("nqk_sgemv_small", ai.vp, bi.vp, ci.vp, 1, K, K)
+        elif M == 1:
+            _lib.call("nqk_sgemv_n", ai.vp, bi.vp, ci.vp, N, K, N, t)
+        else:
+            _lib.call("nqk_sgemv_t", bi.vp, ai.vp, ci.vp, M, K, K, t)
+    return c
+
+
+def sgemv_n(x: DeviceArray, b: DeviceArray) -> DeviceArray:
+    """y[1, N] = x[1, K] . b[K, N] (b row-major) in OpenBLAS GEMV-N order (nqk_sgemv_n)."""
+    K, N = b.shape
+    if x.size != K:
+        raise ValueError(f"matmul: mismatch in core dimension ({x.size} vs {K})")
+    y = DeviceArray((1, N), np.float32)
+    _lib.call("nqk_sgemv_n", x.vp, b.vp, y.vp, N, K, N, openblas_threads())
+    return y
 
 
 # ----------------------------------------------------------------------------- float ops

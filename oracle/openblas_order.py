@@ -135,10 +135,7 @@ def _chunk(a, x, y):
         if (n - n4) & 2:
             y[n4:n4 + 2] = _f(y[n4:n4 + 2] + _k4x2(blk[:, n4:n4 + 2], xb))
         if (n - n4) & 1:
-            if m == 4:  # K = 4: the single leftover column is one multiply-add chain
-                y[n - 1:n] = _f(y[n - 1:n] + _chain(xb, blk[:, n - 1:n].T, False))
-            else:
-                y[n - 1:n] = _f(y[n - 1:n] + _k4x1(blk[:, n - 1:n], xb))
+            y[n - 1:n] = _f(y[n - 1:n] + _k4x1(blk[:, n - 1:n], xb))
         k0 += nb
     if m3:
         # K % 4 trailing rows in C with GCC's fma contraction: one row is
@@ -180,6 +177,9 @@ def sgemv_t(b_t: np.ndarray, x: np.ndarray, threads: int | None = None) -> np.nd
     y = np.zeros(n, np.float32)
     a = np.ascontiguousarray(b_t.T)  # [K, N]
     for j0, j1 in thread_ranges(n, m, threads):
+        if 2 <= m <= SMALL_M and j1 - j0 <= SMALL_N:  # OpenBLAS's small-m kernels (below)
+            y[j0:j1] = _small_chunk(b_t[j0:j1], x)
+            continue
         yc = y[j0:j1].copy()
         _chunk(a[:, j0:j1], x, yc)
         y[j0:j1] = yc
@@ -187,25 +187,57 @@ def sgemv_t(b_t: np.ndarray, x: np.ndarray, threads: int | None = None) -> np.nd
 
 
 # --------------------------------------------------------------------------------------
-# The one-row products outside the GEMV-T kernels above, identified against np.matmul in
-# this container (tests/test_host.py::test_small_one_row_orders_match_numpy_matmul):
-#  * a 1 x 1 result goes to cblas_sdot: below 32 rows the f32 products are summed in double
-#    in order and the sum rounded once (sdot's scalar tail; from 32 rows a vector kernel
-#    whose order is not restated);
-#  * K in 2..8 except 4 goes to OpenBLAS's small-m GEMV-T kernels: columns in blocks of 16
-#    (K = 2), 4 (K = 5) or 8 (K = 3, 6, 7) are k-ordered fma chains, leftover columns
-#    multiply-add chains, except a leftover 4-column block (K = 3, 6, 7) and a last odd
-#    column (K = 3), and K = 8 altogether, whose orders are not restated;
-#  * K = 4: the GEMV-T kernels above, except a single leftover column (N odd), which is a
-#    multiply-add chain.
+# The one-row products outside the kernels above (round 6: every class identified against
+# np.matmul in this container by probing the summation tree of single outputs — which pairs of
+# products meet before a third, with exactly representable inputs — and then which nodes fuse
+# the product into an fma, on random inputs; pinned by tests/test_host.py
+# ::test_small_one_row_orders_match_numpy_matmul and ::test_sdot_order_matches_numpy_matmul):
+#  * a 1 x 1 result goes to cblas_sdot (kernel/x86_64/sdot.c + its SkylakeX micro-kernel): the
+#    first n & -32 elements by the vector kernel — four 16-lane fma accumulators over 64-element
+#    steps, each folded to 8 lanes (low half + high half), four 8-lane fma accumulators over the
+#    remaining 32-element steps, ((a0 + a1) + a2) + a3, low + high 4 lanes, two horizontal adds
+#    — then the f32 products of the tail added in double and the sum rounded once;
+#  * GEMV-T with K = m <= 8 rows and contiguous columns: per thread chunk of at most 16 384
+#    columns (wider chunks: the regular kernels above), OpenBLAS's small-m kernels, whose
+#    column classes (by the column's place in its chunk) are, with p_k = RN(x_k w_k):
+#      F  k-ordered fma chain;  M  multiply-add chain ((p0 + p1) + p2) + ...;
+#      K = 2: F in blocks of 16, the rest M;   K = 5: F in blocks of 4, the rest M;
+#      K = 4: (p0 + p1) + (p2 + p3), a last odd column M;
+#      K = 3: F in blocks of 8; then a 4-column block and a last odd column
+#             fma(x2, w2, fma(x0, w0, p1)); two leftover columns M;
+#      K = 6: F in blocks of 8; a 4-column block (p0 + fma(x1, w1, p2)) + (p3 + fma(x4, w4, p5)); rest M;
+#      K = 7: F in blocks of 8; a 4-column block (fma(x0, w0, p1) + fma(x4, w4, p5)) +
+#             (fma(x2, w2, p3) + p6); rest M;
+#      K = 8: blocks of 4 ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)); two leftover columns
+#             ((p0 + p1) + (p4 + p5)) + ((p2 + p3) + (p6 + p7)); a last odd column
+#             (((p0 + p4) + (p1 + p5)) + (p2 + p6)) + (p3 + p7).
+SMALL_M, SMALL_N = 8, 16384
 
 
 def sdot(x: np.ndarray, w: np.ndarray) -> np.float32:
-    """x . w for a 1 x 1 matmul result (len < 32)."""
-    p = (np.asarray(x, np.float32) * np.asarray(w, np.float32)).astype(np.float32)
+    """x . w for a 1 x 1 matmul result (cblas_sdot's order, any length)."""
+    x = np.asarray(x, np.float32)
+    w = np.asarray(w, np.float32)
+    n = x.size
+    n1 = n & -32
     d = 0.0
-    for v in p:
-        d += float(v)
+    if n1:
+        acc = np.zeros((4, 16), np.float32)
+        i, n64 = 0, n & ~63
+        while i < n64:
+            for q in range(4):
+                acc[q] = _fma(x[i + 16 * q:i + 16 * q + 16], w[i + 16 * q:i + 16 * q + 16], acc[q])
+            i += 64
+        a8 = _f(acc[:, :8] + acc[:, 8:])
+        while i < n1:
+            for q in range(4):
+                a8[q] = _fma(x[i + 8 * q:i + 8 * q + 8], w[i + 8 * q:i + 8 * q + 8], a8[q])
+            i += 32
+        s8 = _f(_f(_f(a8[0] + a8[1]) + a8[2]) + a8[3])
+        h = _f(s8[:4] + s8[4:])
+        d = float(_f(_f(h[0] + h[1]) + _f(h[2] + h[3])))
+    for k in range(n1, n):
+        d += float(_mul(x[k:k + 1], w[k:k + 1])[0])
     return np.float32(d)
 
 
@@ -218,26 +250,151 @@ def _chain(x, w, fma: bool):
 
 
 def small_modes(N: int, K: int) -> str:
-    """Per column: 'F' fma chain, 'M' multiply-add chain, '?' not restated (K in 2..8, not 4)."""
-    blk = 16 if K == 2 else (4 if K == 5 else 8)
-    f_end = N // blk * blk
+    """Per column of a chunk of N columns, the small-m kernel's class for K in 2..8: 'F' fma
+    chain, 'M' multiply-add chain, 'P' K = 4's pairs, 'b' the 4-column block of K = 3, 6, 7
+    (and K = 3's last odd column), 'c' / 'a' / 'e' K = 8's 4-column blocks / two leftover
+    columns / last odd column."""
+    if K == 4:
+        return "P" * (N & ~1) + ("M" if N & 1 else "")
     if K == 8:
-        return "?" * N
-    tail = ""
+        n4 = N & ~3
+        return "c" * n4 + ("aa" if N & 2 else "") + ("e" if N & 1 else "")
+    blk = {2: 16, 5: 4}.get(K, 8)
+    f_end = N // blk * blk
     r = N - f_end
+    tail = ""
     if K in (3, 6, 7) and r >= 4:
-        tail, r = "????", r - 4
+        tail, r = "bbbb", r - 4
     if K == 3:
-        tail += ("MM" if r & 2 else "") + ("?" if r & 1 else "")
+        tail += ("MM" if r & 2 else "") + ("b" if r & 1 else "")
     else:
         tail += "M" * r
     return "F" * f_end + tail
 
 
-def sgemv_small(b_t: np.ndarray, x: np.ndarray) -> np.ndarray:
-    """y = b_t . x for K in 2..8 except 4 ('?' columns computed as fma chains)."""
-    b_t = np.asarray(b_t, np.float32)
-    x = np.asarray(x, np.float32)
+def _small_class(c: str, x, W) -> np.ndarray:
+    K = x.size
+    p = [_mul(np.broadcast_to(x[k], W.shape[:1]), W[:, k]) for k in range(K)]
+    F = lambda k, acc: _fma(np.broadcast_to(x[k], W.shape[:1]), W[:, k], acc)
+    if c == "F":
+        return _chain(x, W, True)
+    if c == "M":
+        return _chain(x, W, False)
+    if c == "P":
+        return _f(_f(p[0] + p[1]) + _f(p[2] + p[3]))
+    if c == "b":
+        if K == 3:
+            return F(2, F(0, p[1]))
+        if K == 6:
+            return _f(_f(p[0] + F(1, p[2])) + _f(p[3] + F(4, p[5])))
+        return _f(_f(F(0, p[1]) + F(4, p[5])) + _f(F(2, p[3]) + p[6]))
+    if c == "c":
+        return _f(_f(_f(p[0] + p[1]) + _f(p[2] + p[3])) + _f(_f(p[4] + p[5]) + _f(p[6] + p[7])))
+    if c == "a":
+        return _f(_f(_f(p[0] + p[1]) + _f(p[4] + p[5])) + _f(_f(p[2] + p[3]) + _f(p[6] + p[7])))
+    return _f(_f(_f(_f(p[0] + p[4]) + _f(p[1] + p[5])) + _f(p[2] + p[6])) + _f(p[3] + p[7]))
+
+
+def _small_chunk(b_t: np.ndarray, x: np.ndarray) -> np.ndarray:
+    """The small-m kernel over one thread chunk b_t [n, K] (K in 2..8)."""
     modes = small_modes(*b_t.shape)
-    fm = np.array([m != "M" for m in modes])
-    return np.where(fm, _chain(x, b_t, True), _chain(x, b_t, False)).astype(np.float32)
+    y = np.zeros(b_t.shape[0], np.float32)
+    for c in set(modes):
+        sel = np.array([m == c for m in modes])
+        y[sel] = _small_class(c, x, b_t[sel])
+    return y
+
+
+def sgemv_small(b_t: np.ndarray, x: np.ndarray, threads: int | None = None) -> np.ndarray:
+    """y = b_t . x for K in 2..8 (= sgemv_t, which dispatches the small-m kernels)."""
+    return sgemv_t(b_t, x, threads)
+
+
+# --------------------------------------------------------------------------------------
+# GEMV-N (round 6): a one-row product x[1, K] @ B[K, N] with B row-major — NumPy's matmul
+# vector_matrix -> cblas_sgemv on the row-major matrix, which OpenBLAS runs as its "N" kernel
+# (kernel/x86_64/sgemv_n_4.c with the SkylakeX micro-kernels, driver/level2/gemv_thread.c);
+# identified against np.matmul in this container as the small-m classes above and pinned by
+# tests/test_host.py::test_sgemv_n_order_matches_numpy_matmul:
+#  * K <= 48: every output a k-ordered fma chain;
+#  * N < 4 (the matrix is its own 1-3 trailing rows, lda == m): t = t + fma(x_k, b_k,
+#    RN(x_{k+1} b_{k+1})) over k = 0, 2, ... below K & -4, then an fma chain over the rest;
+#  * else: the N outputs split over the threads like GEMV-T's columns (thread_ranges); per chunk
+#    of w outputs the last w & 3 are fma chains; the others go in blocks of 4096 outputs (the
+#    last (w & 4095) - (w & 3)); in a block of NB the first NB % 16 outputs take the 8- / 4-row
+#    kernel — per group of 8 products two fma chains (even, odd positions) added, y += a + b;
+#    a leftover group of 4 the same; of 2 or 1 one chain — and the rest the 16-row kernel: per
+#    group of 8, 4, 2, 1 products one fma chain, y += chain.
+
+
+def _bx(x, k, n):
+    return np.broadcast_to(np.float32(x[k]), (n,))
+
+
+def _chain_n(x, b, k0, k1, init=None):
+    acc = np.zeros(b.shape[1], np.float32) if init is None else init
+    for k in range(k0, k1):
+        acc = _fma(_bx(x, k, b.shape[1]), b[k], acc)
+    return acc
+
+
+def _two_acc(x, b, k0, size):
+    n = b.shape[1]
+    a = np.zeros(n, np.float32)
+    e = np.zeros(n, np.float32)
+    for q in range(size):
+        if q & 1:
+            e = _fma(_bx(x, k0 + q, n), b[k0 + q], e)
+        else:
+            a = _fma(_bx(x, k0 + q, n), b[k0 + q], a)
+    return _f(a + e)
+
+
+def _gemv_n_rows(x, b, two: bool):
+    K, n = b.shape
+    y = np.zeros(n, np.float32)
+    for g in range(0, K - K % 8, 8):
+        y = _f(y + (_two_acc(x, b, g, 8) if two else _chain_n(x, b, g, g + 8)))
+    k = K - K % 8
+    for size in (4, 2, 1):
+        if (K % 8) & size:
+            y = _f(y + (_two_acc(x, b, k, size) if (two and size == 4) else _chain_n(x, b, k, k + size)))
+            k += size
+    return y
+
+
+def sgemv_n(b: np.ndarray, x: np.ndarray, threads: int | None = None) -> np.ndarray:
+    """y = x @ b in OpenBLAS GEMV-N's order (b: [K, N] float32 row-major; x: [K])."""
+    b = np.asarray(b, np.float32)
+    x = np.asarray(x, np.float32)
+    K, N = b.shape
+    threads = openblas_threads() if threads is None else threads
+    if K <= 48:
+        return _chain_n(x, b, 0, K)
+    if N < 4:
+        t = np.zeros(N, np.float32)
+        k = 0
+        while k < (K & -4):
+            t = _f(t + _fma(_bx(x, k, N), b[k], _mul(_bx(x, k + 1, N), b[k + 1])))
+            k += 2
+        return _chain_n(x, b, k, K, init=t)
+    y = np.zeros(N, np.float32)
+    for r0, r1 in thread_ranges(N, K, threads):
+        w = r1 - r0
+        m3 = w & 3
+        m1 = w & -4
+        m2 = (w & (NBMAX - 1)) - m3
+        nb, p = NBMAX, r0
+        while nb == NBMAX:
+            m1 -= nb
+            if m1 < 0:
+                if m2 == 0:
+                    break
+                nb = m2
+            r = nb % 16
+            y[p:p + r] = _gemv_n_rows(x, b[:, p:p + r], True)
+            y[p + r:p + nb] = _gemv_n_rows(x, b[:, p + r:p + nb], False)
+            p += nb
+        if m3:
+            y[r1 - m3:r1] = _chain_n(x, b[:, r1 - m3:r1], 0, K)
+    return y

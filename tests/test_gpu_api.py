@@ -129,31 +129,34 @@ def test_profile_dicts_have_the_reference_keys():
 
 
 def test_one_row_kernels_match_numpy_matmul():
-    """nqk_sgemv_small (sdot, K in 2..8 except 4) and nqk_sgemv_t at K = 4 with an odd
-    column count equal the oracle's restatement of NumPy's orders on every column it
-    restates (oracle/openblas_order.py, pinned against np.matmul in the build container by
-    tests/test_host.py; the GPU box's own NumPy may run other OpenBLAS kernels)."""
+    """nqk_sgemv_small (cblas_sdot, every length: the vector kernel from 32 elements) and
+    nqk_sgemv_t (GEMV-T: the small-m kernels for K <= 8 per thread chunk of at most 16 384
+    columns, the regular kernels otherwise) equal the oracle's restatement of NumPy's orders on
+    every column (oracle/openblas_order.py, pinned against np.matmul in the build container by
+    tests/test_host.py; the GPU box's own NumPy may run other OpenBLAS kernels), at OpenBLAS
+    thread counts 1 and 8 (chunks straddling 16 384 columns included)."""
     from numpy_quant import kernels as K
     from numpy_quant.device import DeviceArray
-    from oracle.openblas_order import sdot, sgemv_small, sgemv_t, small_modes
+    from oracle.openblas_order import sdot, sgemv_t
     rng = np.random.default_rng(31)
-    for k in (1, 2, 3, 4, 5, 6, 7, 9, 20, 31):
-        for n in (1, 2, 3, 5, 7, 12, 16, 19, 37, 70):
-            if n == 1 and k >= 32:
-                continue
-            x = rng.standard_normal((1, k)).astype(np.float32)
-            w = rng.standard_normal((n, k)).astype(np.float32)
-            if n == 1:
-                ref = np.array([sdot(x[0], w[0])], np.float32)
-            elif K.small_one_row(n, k):
-                ref = sgemv_small(w, x[0])
-            else:
-                ref = sgemv_t(w, x[0], 1)
-            xd, wd = DeviceArray.from_host(x), DeviceArray.from_host(w)
-            if K.small_one_row(n, k):
-                got = K.sgemv_small(xd, wd).to_host()[0]
-                ok = np.ones(n, bool) if n == 1 else np.array([m != "?" for m in small_modes(n, k)])
-            else:
-                got = K.sgemv_t(xd, wd).to_host()[0]
-                ok = np.ones(n, bool)
-            np.testing.assert_array_equal(got[ok].view(np.int32), ref[ok].view(np.int32), err_msg=f"K={k} N={n}")
+    cases = [(k, n) for k in (1, 2, 3, 4, 5, 6, 7, 8, 9, 20, 31) for n in (1, 2, 3, 5, 7, 12, 16, 19, 37, 70)]
+    cases += [(k, 1) for k in (32, 33, 63, 64, 65, 97, 768, 3072, 10001)]
+    cases += [(k, n) for k in (2, 3, 4, 7, 8) for n in (16385, 60001, 131075)]
+    old = K.BLAS_THREADS
+    try:
+        for threads in (1, 8):
+            K.BLAS_THREADS = threads
+            for k, n in cases:
+                x = rng.standard_normal((1, k)).astype(np.float32)
+                w = rng.standard_normal((n, k)).astype(np.float32)
+                xd, wd = DeviceArray.from_host(x), DeviceArray.from_host(w)
+                if n == 1:
+                    ref = np.array([sdot(x[0], w[0])], np.float32)
+                    got = K.sgemv_small(xd, wd).to_host()[0]
+                else:
+                    ref = sgemv_t(w, x[0], threads)
+                    got = K.sgemv_t(xd, wd).to_host()[0]
+                np.testing.assert_array_equal(got.view(np.int32), ref.view(np.int32),
+                                              err_msg=f"K={k} N={n} threads={threads}")
+    finally:
+        K.BLAS_THREADS = old

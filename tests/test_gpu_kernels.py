@@ -218,6 +218,60 @@ def test_one_row_gemm_takes_gemv_order():
     np.testing.assert_array_equal(y1, (sgemv_t(w, x1[0], 8) + b)[None, :])
 
 
+@pytest.mark.parametrize("K,N,threads", [(49, 2, 8), (64, 3, 1), (3072, 2, 8), (16, 4100, 8), (48, 9000, 8),
+                                         (49, 4100, 1), (64, 9000, 3), (768, 4095, 8), (49, 12289, 8), (768, 700, 2),
+                                         (768, 3072, 8), (3072, 768, 8), (57, 8191, 1), (200, 4099, 8), (5000, 7, 1),
+                                         (100, 5, 8), (59, 36, 1), (63, 28, 8), (2, 40, 8), (1025, 3000, 64)])
+def test_sgemv_n_matches_openblas_order(K, N, threads):
+    """nqk_sgemv_n (one-row float product against a row-major matrix: a MatMul on one row,
+    tensor.py:100-101 -> np.matmul -> OpenBLAS GEMV-N; round 6) equals the oracle's restatement
+    (oracle/openblas_order.py sgemv_n, pinned to np.matmul by tests/test_host.py) bit for bit:
+    every regime (K <= 48 chains, N < 4 pairs, 8- / 16-row kernels, 4096-output blocks, trailing
+    outputs, thread chunks)."""
+    from numpy_quant import kernels as KM
+    from numpy_quant.device import DeviceArray
+    from oracle.openblas_order import sgemv_n
+    rng = np.random.default_rng(K + 7 * N)
+    x = rng.standard_normal(K).astype(np.float32)
+    b = rng.standard_normal((K, N)).astype(np.float32)
+    old = KM.BLAS_THREADS
+    KM.BLAS_THREADS = threads
+    try:
+        got = KM.sgemv_n(DeviceArray.from_host(x[None, :]), DeviceArray.from_host(b)).to_host()[0]
+    finally:
+        KM.BLAS_THREADS = old
+    np.testing.assert_array_equal(got.view(np.int32), sgemv_n(b, x, threads).view(np.int32))
+
+
+def test_matmul_level2_products_take_blas2_orders():
+    """FTensor.matmul (tensor.py:100-101 -> np.matmul) where a product has a vector side: vector
+    @ matrix (GEMV-N), matrix @ vector (GEMV-T over the matrix's rows), vector @ vector (sdot),
+    2-D and stacked (a batch of one-row products against one broadcast weight) — each equal to
+    the oracle's restatement of NumPy's BLAS call, bit for bit."""
+    from numpy_quant import kernels as KM
+    from numpy_quant.device import DeviceArray
+    from oracle.openblas_order import sdot, sgemv_n, sgemv_t
+    rng = np.random.default_rng(12)
+    t = KM.openblas_threads()
+    for K, N in ((768, 3072), (64, 10), (33, 5), (100, 2)):
+        x = rng.standard_normal((1, K)).astype(np.float32)
+        b = rng.standard_normal((K, N)).astype(np.float32)
+        got = KM.matmul_f32(DeviceArray.from_host(x), DeviceArray.from_host(b)).to_host()
+        np.testing.assert_array_equal(got[0].view(np.int32), sgemv_n(b, x[0], t).view(np.int32), err_msg=f"{K} {N}")
+        a = rng.standard_normal((N, K)).astype(np.float32)
+        v = rng.standard_normal((K, 1)).astype(np.float32)
+        got = KM.matmul_f32(DeviceArray.from_host(a), DeviceArray.from_host(v)).to_host()
+        np.testing.assert_array_equal(got[:, 0].view(np.int32), sgemv_t(a, v[:, 0], t).view(np.int32), err_msg=f"mv {K} {N}")
+        got = KM.matmul_f32(DeviceArray.from_host(x), DeviceArray.from_host(v)).to_host()
+        assert got.shape == (1, 1) and got[0, 0].view(np.int32) == sdot(x[0], v[:, 0]).view(np.int32)
+    xs = rng.standard_normal((3, 1, 96)).astype(np.float32)
+    b = rng.standard_normal((96, 40)).astype(np.float32)
+    got = KM.matmul_f32(DeviceArray.from_host(xs), DeviceArray.from_host(b)).to_host()
+    assert got.shape == (3, 1, 40)
+    for i in range(3):
+        np.testing.assert_array_equal(got[i, 0].view(np.int32), sgemv_n(b, xs[i, 0], t).view(np.int32))
+
+
 @pytest.mark.parametrize("M,N,K", [(1000, 768, 768), (197, 192, 768), (130, 260, 64), (50176 // 16, 768, 768)])
 def test_sgemm_vector_loads_equal_scalar_loads(M, N, K, monkeypatch):
     """k_sgemm_mfma's 16-byte operand loads (unit-stride A rows and B rows) give the same

@@ -94,11 +94,12 @@ def ref_qparams(meta_qp):
 
 def tainted_values(model):
     """Values downstream of a float one-row product (M = 1) whose OpenBLAS order is not
-    reproduced: a one-row Gemm against a transposed weight goes to OpenBLAS GEMV-T (or its
-    small-m kernels, or sdot for one column), which nqk_sgemv_t / nqk_sgemv_small reproduce
-    where kernels.one_row_restated says so (oracle/openblas_order.py); GEMV-N (a one-row
-    MatMul against a row-major weight) is not restated, so values downstream of it may
-    differ by ulps.  Every GEMM with M > 1, any K, is reproduced (OpenBLAS's GEMM_Q = 448 K blocks)."""
+    reproduced.  Since round 6 every one is (kernels.one_row_restated): a one-row Gemm against a
+    transposed weight goes to OpenBLAS GEMV-T (its regular or small-m kernels) or sdot for one
+    column (nqk_sgemv_t / nqk_sgemv_small), a one-row MatMul against a row-major weight to GEMV-N
+    (nqk_sgemv_n), all restated in oracle/openblas_order.py; every GEMM with M > 1, any K, is
+    reproduced (OpenBLAS's GEMM_Q = 448 K blocks).  So the set is empty unless
+    one_row_restated says otherwise."""
     from numpy_quant.kernels import one_row_restated
     bad = set()
     for node in model.nodes:
@@ -110,8 +111,7 @@ def tainted_values(model):
                 gemm_t = (node.op == "Gemm" and node.attrs.get("transB") and not node.attrs.get("transA")
                           and a.dev.ndim == 2 and w.dev.ndim == 2)
                 n = w.dev.shape[0] if gemm_t else w.dev.shape[-1]
-                covered = ((gemm_t and one_row_restated(w.dev.shape[0], a.dev.shape[1]))
-                           or (a.dev.ndim == 2 and w.dev.ndim == 2 and n == 1 and a.dev.shape[1] < 32))
+                covered = one_row_restated(n, a.dev.shape[-1])
                 if not covered:
                     bad.update(o.name for o in node.outputs)
         if any(i in bad for i in ins):

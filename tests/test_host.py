@@ -206,42 +206,77 @@ def test_sgemv_order_matches_numpy_matmul(K, N, threads):
     np.testing.assert_array_equal(sgemv_t(w, x, threads).view(np.int32), ref.view(np.int32))
 
 
-@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 31])
-def test_small_one_row_orders_match_numpy_matmul(K):
-    """The one-row products outside the GEMV-T restatement (oracle/openblas_order.py
-    sdot / sgemv_small, K = 4's leftover column): every column the oracle calls restated
-    equals np.matmul bit for bit, for N = 1 (sdot) and N = 2..70; and
-    kernels.one_row_restated (what the product reports) says restated exactly where the
-    oracle has no '?' column."""
+def _openblas_haswell_family():
     threadpoolctl = pytest.importorskip("threadpoolctl")
     info = [i for i in threadpoolctl.threadpool_info() if i.get("internal_api") == "openblas"]
     if not info or info[0].get("architecture") not in ("Haswell", "Zen", "SkylakeX", "Cooperlake", "SapphireRapids"):
         pytest.skip("OpenBLAS does not run its Haswell-family GEMV kernels on this host")
-    from oracle.openblas_order import sdot, sgemv_small, sgemv_t, small_modes
-    from numpy_quant.kernels import one_row_restated, small_one_row
+    return threadpoolctl
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 31])
+def test_small_one_row_orders_match_numpy_matmul(K):
+    """oracle/openblas_order.py's GEMV-T for K <= 8 (OpenBLAS's small-m kernels per thread chunk
+    of at most 16 384 columns, the regular kernels for wider chunks; round 6 identified every
+    column class) equals np.matmul bit for bit on every column: N = 2..70 and chunks around
+    16 384 columns at OpenBLAS thread counts 1, 3 and 8; kernels.one_row_restated says so."""
+    threadpoolctl = _openblas_haswell_family()
+    from oracle.openblas_order import sgemv_t
+    from numpy_quant.kernels import one_row_restated
     rng = np.random.default_rng(1000 + K)
-    for N in list(range(1, 41)) + [63, 70]:
-        for _ in range(6):
+    big = [16383, 16384, 16385, 57601, 70001, 131075] if K <= 8 else [20001]
+    for threads in (1, 3, 8):
+        for N in (list(range(2, 71)) if threads == 8 else [2, 5, 37, 70]) + big:
             x = rng.standard_normal(K).astype(np.float32)
             w = rng.standard_normal((N, K)).astype(np.float32)
-            ref = (x[None, :] @ w.T)[0]
-            if N == 1:
-                if K < 32:
-                    assert sdot(x, w[0]).view(np.int32) == ref.view(np.int32)[0], (K, N)
-                assert one_row_restated(N, K) == (K < 32)
-                continue
-            if small_one_row(N, K):
-                modes = small_modes(N, K)
-                got = sgemv_small(w, x)
-                ok = np.array([m != "?" for m in modes])
-                np.testing.assert_array_equal(got[ok].view(np.int32), ref[ok].view(np.int32), err_msg=f"K={K} N={N}")
-                assert one_row_restated(N, K) == bool(ok.all()), (K, N, modes)
-            else:
-                with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
-                    ref1 = (x[None, :] @ w.T)[0]
-                np.testing.assert_array_equal(sgemv_t(w, x, 1).view(np.int32), ref1.view(np.int32),
-                                              err_msg=f"K={K} N={N}")
-                assert one_row_restated(N, K)
+            with threadpoolctl.threadpool_limits(limits=threads, user_api="blas"):
+                ref = (x[None, :] @ w.T)[0]
+            np.testing.assert_array_equal(sgemv_t(w, x, threads).view(np.int32), ref.view(np.int32),
+                                          err_msg=f"K={K} N={N} threads={threads}")
+            assert one_row_restated(N, K)
+
+
+def test_sdot_order_matches_numpy_matmul():
+    """oracle/openblas_order.py sdot (cblas_sdot: the SkylakeX vector kernel's accumulators
+    from 32 elements, the tail in double) equals np.matmul's 1 x 1 product bit for bit at every
+    length class (below 32, 32-element steps, 64-element steps, ragged tails, 4 M elements)."""
+    threadpoolctl = _openblas_haswell_family()
+    from oracle.openblas_order import sdot
+    rng = np.random.default_rng(77)
+    for n in list(range(1, 200)) + [255, 256, 257, 768, 3072, 4099, 65537, 1 << 22]:
+        x = rng.standard_normal(n).astype(np.float32)
+        w = rng.standard_normal(n).astype(np.float32)
+        for threads in ((1, 8) if n > 10000 else (8,)):
+            with threadpoolctl.threadpool_limits(limits=threads, user_api="blas"):
+                ref = np.matmul(x[None, :], w[:, None])[0, 0]
+            assert sdot(x, w).view(np.int32) == ref.view(np.int32), (n, threads)
+
+
+_GEMV_N_CASES = [(49, 2), (64, 3), (3072, 2), (16, 4100), (48, 9000), (49, 4100), (64, 9000), (768, 4095),
+                 (49, 12289), (768, 700), (768, 3072), (3072, 768), (57, 8191), (200, 4099), (5000, 7), (100, 5),
+                 (50, 16), (59, 36), (63, 28), (2, 40), (9, 33)]
+
+
+@pytest.mark.parametrize("K,N", _GEMV_N_CASES)
+def test_sgemv_n_order_matches_numpy_matmul(K, N):
+    """oracle/openblas_order.py sgemv_n (round 6: OpenBLAS GEMV-N for a one-row product against
+    a row-major matrix — K <= 48 fma chains, N < 4 pairs, the 8- / 16-row kernels' groups of 8
+    per block of 4096 outputs, trailing outputs, the thread split) equals np.matmul bit for bit
+    at OpenBLAS thread counts 1, 3 and 8; and matrix @ vector equals GEMV-T over the matrix's
+    rows (sgemv_t)."""
+    threadpoolctl = _openblas_haswell_family()
+    from oracle.openblas_order import sgemv_n, sgemv_t
+    rng = np.random.default_rng(K * 131 + N)
+    for threads in (1, 3, 8):
+        b = rng.standard_normal((K, N)).astype(np.float32)
+        x = rng.standard_normal(K).astype(np.float32)
+        with threadpoolctl.threadpool_limits(limits=threads, user_api="blas"):
+            ref = np.matmul(x[None, :], b)[0]
+            ref_mv = np.matmul(b.T.copy(), x[:, None])[:, 0]  # matrix [N, K] @ vector
+        np.testing.assert_array_equal(sgemv_n(b, x, threads).view(np.int32), ref.view(np.int32),
+                                      err_msg=f"K={K} N={N} threads={threads}")
+        np.testing.assert_array_equal(sgemv_t(b.T.copy(), x, threads).view(np.int32), ref_mv.view(np.int32),
+                                      err_msg=f"matrix @ vector K={K} N={N} threads={threads}")
 
 
 def test_redimension_vit_base_to_tiny():
