@@ -239,12 +239,16 @@ def host_cpu() -> dict:
     return {"cpu_model": model, "nproc": os.cpu_count()}
 
 
-def cpu_baseline_vit(bit_width: int, tiny: bool = False, mode: str = "full") -> dict:
+def cpu_baseline_vit(bit_width: int, tiny: bool = False, mode: str = "full", qmodel=None, x0=None,
+                     out0=None) -> dict:
     """The oracle (CPU restatement of the reference's QModel.__call__, int64 np.matmul) on a
     bounded sample of the same workload.  mode "full" (default, BASELINE.md's plan): the whole
     classifier forward (patch embedding, 12 encoder layers, classifier) on ONE image, measured
     (~30 s for ViT-Base on one core); mode "layer": one encoder layer at batch 1, x12
-    (extrapolated: drops the embedding and the classifier, ~3 s)."""
+    (extrapolated: drops the embedding and the classifier, ~3 s).  With qmodel / x0 / out0
+    (round 6), the full forward runs on the bench's own image 0 with the device calibration's
+    quantization parameters (oracle quantize_with), and its logits are compared with the
+    device's row 0: an oracle check of the timed output independent of the node loop."""
     import numpy as np
     from numpy_quant import onnx_proto
     from oracle import nq_oracle as O
@@ -261,11 +265,24 @@ def cpu_baseline_vit(bit_width: int, tiny: bool = False, mode: str = "full") -> 
             onnx_proto.redimension(proto, *VIT_TINY)
         x = rng.standard_normal((1, 3, 224, 224)).astype(np.float32)
     g = O.Graph(proto)
+    check = None
     with np.errstate(all="ignore"):
-        qp, qc = O.calibrate(g, [x], bit_width)
+        if mode == "full" and qmodel is not None:
+            x = np.asarray(x0, np.float32)[None]
+            qp, qc = O.quantize_with(g, {k: O.QParams(v.scale, v.zero_point) for k, v in qmodel.quant_params.items()},
+                                     bit_width)
+        else:
+            qp, qc = O.calibrate(g, [x], bit_width)
         t0 = time.perf_counter()
-        O.quantized_forward(g, qp, qc, [x], bit_width)
+        vals = O.quantized_forward(g, qp, qc, [x], bit_width)
         dt = time.perf_counter() - t0
+    if mode == "full" and qmodel is not None:
+        ref = O.outputs_of(g, vals)[0][0]
+        got = np.asarray(out0)
+        check = {"image": 0, "equal": bool(np.array_equal(ref.view(np.int32), got.view(np.int32))),
+                 "max_abs_diff": float(np.max(np.abs(ref.astype(np.float64) - got))),
+                 "against": "oracle/nq_oracle.py QModel forward of the bench's image 0 with the device "
+                            "calibration's quantization parameters (quantize_with), every logit"}
     if mode == "layer":
         per_image = 12 * dt
         sample = (f"EXTRAPOLATED: oracle QModel forward of 1 ViT-{arch} encoder layer, batch 1 ({dt:.1f} s), x12 layers "
@@ -276,6 +293,9 @@ def cpu_baseline_vit(bit_width: int, tiny: bool = False, mode: str = "full") -> 
                   f"layers, classifier) on 1 image, {dt:.1f} s")
     res = {"value": 1.0 / per_image, "unit": "samples/s", "cores": 1, "kind": "port",
            "sample": sample + "; int64 np.matmul is single-threaded (99% of the time)"}
+    if check is not None:
+        res["sample"] += "; the bench's own image 0 with the device calibration's parameters"
+        res["oracle_check"] = check
     res.update(host_cpu())
     return res
 
@@ -400,7 +420,10 @@ def run_vit(args, group):
     res["kernels"] = kern
     res.update(ver)
     if not args.no_cpu_baseline and world == 1:
-        res["cpu_baseline"] = cpu_baseline_vit(bw, tiny, args.cpu_baseline)
+        res["cpu_baseline"] = cpu_baseline_vit(bw, tiny, args.cpu_baseline, qmodel, x[0], out_host[0])
+        oc = res["cpu_baseline"].pop("oracle_check", None)
+        if oc is not None:
+            res["oracle_check"] = oc
     return res
 
 

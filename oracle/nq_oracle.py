@@ -426,6 +426,33 @@ def calibrate(graph: Graph, calibration_inputs: list[np.ndarray], bit_width: int
     return qp, qconst
 
 
+def quantize_with(graph: Graph, qparams: dict, bit_width: int = 8):
+    """Model.quantize's constant handling (model.py:328-442, as calibrate above) for GIVEN
+    per-value parameters (e.g. another implementation's calibration): every constant quantized
+    with its own parameters, Gemm biases and constants added to a value at 4 * bit_width with
+    the product / input scale.  Returns (qparams, qconstants)."""
+    qp = dict(qparams)
+    qconst: dict[str, tuple] = {}
+    for name, arr in graph.constants.items():
+        p = qp[name]
+        qconst[name] = Q(quantize(arr, bit_width, p.scale, p.zero_point), bit_width, p.scale, p.zero_point)
+    is_const = set(graph.constants)
+    for _, op, _, ins, outs in graph.nodes:
+        if op == "Gemm":
+            bias = ins[2]
+            bscale = qp[ins[0]].scale * qp[ins[1]].scale
+            qp[bias] = QParams(bscale, None)
+            qconst[bias] = Q(quantize(graph.constants[bias], 4 * bit_width, bscale, None),
+                             4 * bit_width, bscale, None)
+        if op == "Add" and (ins[0] in is_const or ins[1] in is_const):
+            bi, xi = (0, 1) if ins[0] in is_const else (1, 0)
+            bscale = qp[ins[xi]].scale
+            qconst[ins[bi]] = Q(quantize(graph.constants[ins[bi]], 4 * bit_width, bscale, None),
+                                4 * bit_width, bscale, None)
+            qp[ins[bi]] = QParams(bscale, None)
+    return qp, qconst
+
+
 def quantized_forward(graph: Graph, qp: dict, qconst: dict, inputs: list[np.ndarray],
                       bit_width: int, profile: bool = False):
     """QModel.__call__, model.py:486-565.  Returns {value: tagged tensor} (and the
