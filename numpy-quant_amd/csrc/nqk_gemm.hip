@@ -427,6 +427,9 @@ constexpr int EQ_ROW = 20;  // floats per LDS operand row (16 + 4 padding)
 #ifndef NQK_EMBED_PXD
 #define NQK_EMBED_PXD 1
 #endif
+#ifndef NQK_EMBED_DIAG
+#define NQK_EMBED_DIAG 0  // timing diagnostics (wrong results): 1 no k-tile barriers, 2 no A convert, 4 no stores
+#endif
 template <int WN>
 __global__ void __launch_bounds__(256, 2)
 k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __restrict__ C, int64_t M, int64_t N,
@@ -491,7 +494,10 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
   };
   auto store_a = [&](int buf, auto SUB, const int4 (&d)[3]) __attribute__((always_inline)) {
     float f[8];
-    if (hf) conv_a(SUB, std::integral_constant<int, 1>{}, d, f);
+    if constexpr ((NQK_EMBED_DIAG & 2) != 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = __int_as_float(d[e % 3].x);
+    } else if (hf) conv_a(SUB, std::integral_constant<int, 1>{}, d, f);
     else conv_a(SUB, std::integral_constant<int, 0>{}, d, f);
     float* dst = &sa[buf][ar * EQ_ROW + 4 * hf];
     *reinterpret_cast<v4f*>(dst) = v4f{f[0], f[2], f[4], f[6]};      // k_local even -> p = k_local / 2
@@ -567,7 +573,7 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
       store_a(cur ^ 1, std::integral_constant<int, (sub + 1) % 3>{}, px);
       store_b(cur ^ 1);
     }
-    __syncthreads();
+    if constexpr ((NQK_EMBED_DIAG & 1) == 0) __syncthreads();
   };
   for (int ki = 0; ki < NKT / 3; ++ki) {
     step(3 * ki, std::integral_constant<int, 0>{});
@@ -599,7 +605,11 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
       const int co = (gm + im + 1) * Ni, po = (gm - im * hwi + 1) * Ni;
 #pragma unroll
       for (int j = 0; j < WN; ++j)
-        if (gnj[j] < Ni) C[co + gnj[j]] = (tot[i][j][r] + bj[j]) + ee.pos[po + gnj[j]];
+        if (gnj[j] < Ni) {
+          const float v = (tot[i][j][r] + bj[j]) + ee.pos[po + gnj[j]];
+          if constexpr ((NQK_EMBED_DIAG & 4) != 0) asm volatile("" ::"v"(v));
+          else C[co + gnj[j]] = v;
+        }
     }
 }
 
