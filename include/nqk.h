@@ -195,6 +195,10 @@ int nqk_patchify_dequant(const int8_t* q, float* cols, int64_t n, int64_t c, int
  * q: int8 [images][3][h][w], 16 x 16 patches; wt: the weights as [N][768] in the
  * (ki, kj, ci) order with every 16-block permuted to p = (k & 1) * 8 + (k >> 1)
  * (numpy_quant/plan.py FusedEmbed); N % 64 == 0. */
+/* The order nqk_embed_q expects its weights in, per 16-k block: 32 -> p = (k & 1) * 8 + (k >> 1) (the
+ * v_mfma_f32_32x32x2_f32 kernel), 16 -> p = (k & 3) * 4 + (k >> 2) (the v_mfma_f32_16x16x4_f32 kernel;
+ * round 6).  Callers permute the weights by it (plan.py FusedEmbed). */
+int nqk_embed_weight_order(void);
 int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float* wt, const float* bias, const float* cls,
                 const float* pos, float* out, int64_t images, int64_t c, int64_t h, int64_t w, int64_t kh,
                 int64_t kw, int64_t N);

@@ -613,6 +613,166 @@ k_embed_q(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __r
     }
 }
 
+// k_embed_q on v_mfma_f32_16x16x4_f32 (round 6).  Same tiles (128 x 64 WN, 4 waves 2 x 2, k-tiles of
+// 16, double-buffered LDS), same numerics: one 16x16x4 instruction accumulates its 4 k-products in
+// order with a rounding after each (an fmaf chain, tools/micro/f32mfma: 0 of 12 800 outputs differ),
+// so every output is still the k-ordered chain per BLAS K block.  Why: the chip holds a higher clock
+// under the 16x16 f32 form than under 32x32x2 with operands from LDS (MI355X_MICROARCH.md, DVFS item 7).
+// A wave's 64 x 32 WN tile is 4 x 2 WN blocks of 16 x 16; lane (l16 = l & 15, g = l >> 4) supplies
+// A[row l16][k0 + g] and B[k0 + g][col l16] for k0 = 0, 4, 8, 12, i.e. k = 4 q + g for q = 0..3: the
+// LDS rows hold each 16-k tile permuted to p = (k & 3) * 4 + (k >> 2), so a lane's four values are one
+// ds_read_b128 (24-float rows: conflict-free in every ds_read_b128 lane group); the weights come in
+// that order (plan.py FusedEmbed, nqk.h).
+constexpr int EQ16_ROW = 24;
+template <int WN>
+__global__ void __launch_bounds__(256, 2)
+k_embed_q16(const int8_t* __restrict__ q, const float* __restrict__ wt, float* __restrict__ C, int64_t M, int64_t N,
+            int64_t hw, int64_t wo, int64_t H, int64_t W, float s, float zpf, KBlocks kb, EmbedEpi ee) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  constexpr int BN = 64 * WN, K = 768, NJ = 2 * WN;
+  __shared__ __attribute__((aligned(16))) float sa[2][128 * EQ16_ROW];
+  __shared__ __attribute__((aligned(16))) float sb[2][BN * EQ16_ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, l16 = lane & 15, g = lane >> 4;
+  int64_t tm = blockIdx.y, tn = blockIdx.x;
+  if (ee.xcd) {  // XCD-aware tile order, as k_embed_q
+    const int64_t gx = gridDim.x, T = gx * gridDim.y, b = (int64_t)blockIdx.y * gx + blockIdx.x;
+    const int64_t XC = ee.xcd, x = b % XC, q8 = T / XC, r8 = T % XC;
+    const int64_t tile = x * q8 + (x < r8 ? x : r8) + b / XC;
+    tm = tile / gx;
+    tn = tile - tm * gx;
+  }
+  const int64_t m0 = tm * 128, n0 = tn * BN;
+  const int ar = tid & 127, hf = tid >> 7;
+  const int64_t am = m0 + ar < M ? m0 + ar : M - 1;
+  const int64_t img = am / hw, pt = am - img * hw, oy = pt / wo, ox = pt - oy * wo;
+  const int8_t* qrow = q + ((img * 3) * H + oy * 16) * W + ox * 16;
+  const int64_t cstride = H * W;
+  int4 px[3], pxn[3];
+  auto load_px = [&](int ki, int4 (&d)[3]) {
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci) d[ci] = *reinterpret_cast<const int4*>(qrow + ci * cstride + (int64_t)ki * W);
+  };
+  const int cb = tid >> 2, kq = tid & 3;
+  v4f bv[WN];
+  auto load_b = [&](int kt) {
+#pragma unroll
+    for (int u = 0; u < WN; ++u) {
+      const int64_t n = n0 + cb + 64 * u;
+      bv[u] = n < N ? *reinterpret_cast<const v4f*>(wt + n * K + kt * 16 + 4 * kq) : v4f{0, 0, 0, 0};
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < WN; ++u) *reinterpret_cast<v4f*>(&sb[buf][(cb + 64 * u) * EQ16_ROW + 4 * kq]) = bv[u];
+  };
+  // A values of k-tile sub: k_local = 8 hf + e, written at p = (e & 3) * 4 + 2 hf + (e >> 2): the
+  // pairs (e, e + 4) are adjacent, four 8-byte stores
+  auto conv_a = [&](auto SUB, auto HF, const int4 (&d)[3], float (&f)[8]) __attribute__((always_inline)) {
+    constexpr int sub = decltype(SUB)::value, half = decltype(HF)::value;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = 16 * sub + 8 * half + e, kj = j / 3, c = j % 3;
+      const int w = (kj >> 2) == 0 ? d[c].x : (kj >> 2) == 1 ? d[c].y : (kj >> 2) == 2 ? d[c].z : d[c].w;
+      f[e] = ((float)(int)(int8_t)(w >> (8 * (kj & 3))) - zpf) * s;
+    }
+  };
+  auto store_a = [&](int buf, auto SUB, const int4 (&d)[3]) __attribute__((always_inline)) {
+    float f[8];
+    if (hf) conv_a(SUB, std::integral_constant<int, 1>{}, d, f);
+    else conv_a(SUB, std::integral_constant<int, 0>{}, d, f);
+    float* dst = &sa[buf][ar * EQ16_ROW + 2 * hf];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) *reinterpret_cast<v2f*>(dst + 4 * e) = v2f{f[e], f[e + 4]};
+  };
+  v4f acc[4][NJ], tot[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = tot[i][j] = v4f{0, 0, 0, 0};
+  int blk = 0;
+  int64_t bend = kb.n > 0 ? kb.end[0] : -1;
+  load_px(0, px);
+  load_b(0);
+  store_a(0, std::integral_constant<int, 0>{}, px);
+  store_b(0);
+  __syncthreads();
+  constexpr int NKT = K / 16;
+  auto step = [&](int kt, auto SUB) __attribute__((always_inline)) {
+    constexpr int sub = decltype(SUB)::value;
+    const int cur = kt & 1;
+    const bool more = kt + 1 < NKT;
+    if (more) load_b(kt + 1);
+    if constexpr (sub == 0) {
+      if (kt + 3 < NKT) load_px(kt / 3 + 1, pxn);
+    }
+    v4f fb[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      fb[j] = *reinterpret_cast<const v4f*>(&sb[cur][(wn * 32 * WN + 16 * j + l16) * EQ16_ROW + 4 * g]);
+    // row block by row block (one A fragment live at a time): 4 NJ MFMAs per block, the NJ
+    // accumulators of a block in rotation
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const v4f fa = *reinterpret_cast<const v4f*>(&sa[cur][(wm * 64 + 16 * i + l16) * EQ16_ROW + 4 * g]);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[qq], fb[j][qq], acc[i][j], 0, 0, 0);
+    }
+    if ((int64_t)kt * 16 + 16 == bend) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          tot[i][j] = tot[i][j] + acc[i][j];
+          acc[i][j] = v4f{0, 0, 0, 0};
+        }
+      ++blk;
+      bend = blk < kb.n ? kb.end[blk] : -1;
+    }
+    if (more) {
+      if constexpr (sub == 2) {
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) px[ci] = pxn[ci];
+      }
+      store_a(cur ^ 1, std::integral_constant<int, (sub + 1) % 3>{}, px);
+      store_b(cur ^ 1);
+    }
+    __syncthreads();
+  };
+  for (int ki = 0; ki < NKT / 3; ++ki) {
+    step(3 * ki, std::integral_constant<int, 0>{});
+    step(3 * ki + 1, std::integral_constant<int, 1>{});
+    step(3 * ki + 2, std::integral_constant<int, 2>{});
+  }
+  // epilogue (as k_embed_q): lane holds rows 16 i + 4 g + r, column 16 j + l16 of the wave tile
+  const int hwi = (int)ee.hw, Ni = (int)N, Mi = (int)M;
+  const float rhw = 1.0f / (float)hwi;
+  float bj[NJ];
+  int gnj[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    gnj[j] = (int)n0 + wn * 32 * WN + 16 * j + l16;
+    bj[j] = gnj[j] < Ni ? ee.bias[gnj[j]] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gm = (int)m0 + wm * 64 + 16 * i + 4 * g + r;
+      if (gm >= Mi) continue;
+      int im = (int)((float)gm * rhw);
+      im = im * hwi > gm ? im - 1 : im;
+      im = (im + 1) * hwi <= gm ? im + 1 : im;
+      const int co = (gm + im + 1) * Ni, po = (gm - im * hwi + 1) * Ni;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if (gnj[j] < Ni) C[co + gnj[j]] = (tot[i][j][r] + bj[j]) + ee.pos[po + gnj[j]];
+    }
+}
+
 // class-token rows of the EMBED output: out[image][0][n] = cls[n] + pos[0][n]
 __global__ void k_embed_cls(const float* __restrict__ cls, const float* __restrict__ pos, float* __restrict__ out,
                             int64_t images, int64_t hw, int64_t n) {
@@ -1100,6 +1260,16 @@ extern "C" int nqk_sgemm_embed(const float* cols, const float* w, const float* b
   return launch_status("nqk_sgemm_embed(cls)");
 }
 
+// which k_embed_q form nqk_embed_q runs, and so the order its weights must come in: 16 = the
+// v_mfma_f32_16x16x4_f32 form (p = (k & 3) * 4 + (k >> 2) in every 16-k block), 32 = the 32x32x2
+// form (p = (k & 1) * 8 + (k >> 1)).  NQK_EMBED_MFMA=16 / 32 selects (A/B; read per call, so a
+// caller must not change it between permuting its weights and launching).
+static bool embed_mfma16() {
+  const char* e = getenv("NQK_EMBED_MFMA");
+  return e && atoi(e) == 16;
+}
+extern "C" int nqk_embed_weight_order(void) { return embed_mfma16() ? 16 : 32; }
+
 extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float* wt, const float* bias,
                            const float* cls, const float* pos, float* out, int64_t images, int64_t c, int64_t h,
                            int64_t w, int64_t kh, int64_t kw, int64_t N) {
@@ -1121,7 +1291,14 @@ extern "C" int nqk_embed_q(const int8_t* q, float scale, int64_t zp, const float
   // profiles/r04_embed_1wg_streams_dropped.txt)
   // (NQK_EMBED_WN1=1: the 128 x 64 tiles at N % 128 == 0 as well — 150 VGPRs, 3 workgroups per CU
   // instead of 2, twice the tiles; round-6 A/B)
-  if (N % 128 == 0 && !getenv("NQK_EMBED_WN1")) {
+  if (embed_mfma16()) {  // the weights in the 16x16 kernel's order (nqk_embed_weight_order() == 16)
+    if (N % 128 == 0 && !getenv("NQK_EMBED_WN1"))
+      hipLaunchKernelGGL(k_embed_q16<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
+                         wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
+    else
+      hipLaunchKernelGGL(k_embed_q16<1>, dim3((unsigned)(N / 64), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
+                         wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
+  } else if (N % 128 == 0 && !getenv("NQK_EMBED_WN1")) {
     hipLaunchKernelGGL(k_embed_q<2>, dim3((unsigned)(N / 128), (unsigned)((M + 127) / 128)), dim3(256), 0, stream(), q,
                        wt, out, M, N, hw, wo, h, w, scale, zpf, kb, EmbedEpi{bias, pos, hw, getenv("NQK_EMBED_NOXCD") ? 0 : num_xcds()});
   } else {

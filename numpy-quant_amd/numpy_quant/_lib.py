@@ -116,6 +116,7 @@ SIGNATURES = {
     "nqk_selftest_gelu_filter": [_p],
     "nqk_sgemm_embed": [_p, _p, _p, _p, _p, _p, _l, _l, _l, _l],
     "nqk_patchify_dequant": [_p, _p, _l, _l, _l, _l, _l, _l, _f, _l],
+    "nqk_embed_weight_order": [],
     "nqk_embed_q": [_p, _f, _l, _p, _p, _p, _p, _p, _l, _l, _l, _l, _l, _l, _l],
     "nqk_comm_unique_id": [_p],
     "nqk_comm_init": [_p, _i, _i],

@@ -429,6 +429,18 @@ class _ShapeOnly:
         return ITensor(np.array(self._shape, dtype=np.int64))
 
 
+def embed_weight_image(W: DeviceArray, kout: int, kk: int) -> DeviceArray:
+    """The Conv weight [kout][c][16][16] as nqk_embed_q's [kout][K] image: K in (ki, kj, ci) order,
+    each 16-k block permuted to the kernel's order (nqk_embed_weight_order, include/nqk.h)."""
+    from .device import permute
+    order = _lib.load().nqk_embed_weight_order()
+    if order == 16:
+        wt = permute(W, [0, 2, 3, 1]).reshape((kout, kk // 16, 4, 4))
+    else:
+        wt = permute(W, [0, 2, 3, 1]).reshape((kout, kk // 16, 8, 2))
+    return permute(wt, [0, 1, 3, 2]).reshape((kout, kk))
+
+
 class FusedEmbed:
     def __init__(self, qmodel, m: EmbedMatch):
         self.m = m
@@ -446,12 +458,12 @@ class FusedEmbed:
             raise NoMatch("embedding dimensions")
         self._cols = None
         # nqk_embed_q (no im2col matrix): 3-channel 16 x 16 patches, N % 64 == 0; the
-        # weights as [N][K] in (ki, kj, ci) order, each 16-block of k permuted to
-        # p = (k & 1) * 8 + (k >> 1) (the kernel's LDS order)
+        # weights as [N][K] in (ki, kj, ci) order, each 16-block of k permuted to the kernel's
+        # LDS order (nqk_embed_weight_order): p = (k & 1) * 8 + (k >> 1) for the 32x32x2 kernel,
+        # p = (k & 3) * 4 + (k >> 2) for the 16x16x4 one
         self.wt = None
         if (cin == 3 and m.kh == 16 and m.kw == 16 and self.kout % 64 == 0 and os.environ.get("NQK_EMBED_Q", "1") != "0"):
-            wt = permute(W, [0, 2, 3, 1]).reshape((self.kout, self.kk // 16, 8, 2))
-            self.wt = permute(wt, [0, 1, 3, 2]).reshape((self.kout, self.kk))
+            self.wt = embed_weight_image(W, self.kout, self.kk)
 
     def pre(self, qmodel):
         """at the Conv's position: the shape-only placeholder for the Shape consumer"""

@@ -141,13 +141,18 @@ def test_patchify_dequant_equals_dequantize_then_im2col(n, c, h, w, kh, kw, zp):
 
 @pytest.mark.parametrize("n,h,w,N,zp", [(3, 224, 224, 768, -5), (2, 224, 224, 192, 0), (1, 32, 48, 64, 17),
                                         (5, 64, 32, 128, -128)])
-def test_embed_q_equals_patchify_then_sgemm_embed(n, h, w, N, zp):
+@pytest.mark.parametrize("mfma", ["32", "16"])
+def test_embed_q_equals_patchify_then_sgemm_embed(n, h, w, N, zp, mfma, monkeypatch):
     """nqk_embed_q (patchify + dequantize folded into the GEMM's A-operand load, round 3)
     gives the bits of nqk_patchify_dequant + nqk_sgemm_embed (the im2col path, pinned to the
     reference's fconv2d by test_gpu_kernels / vit_b1): bias, position embedding and the
-    class-token rows included; ragged last row tile (n * hw % 128 != 0) and N = 64 / 192."""
+    class-token rows included; ragged last row tile (n * hw % 128 != 0) and N = 64 / 192;
+    both kernel forms (v_mfma_f32_32x32x2_f32 and, round 6, 16x16x4), each with its weight
+    order (plan.embed_weight_image)."""
+    monkeypatch.setenv("NQK_EMBED_MFMA", mfma)
     from numpy_quant import _lib
     from numpy_quant.device import DeviceArray, permute
+    from numpy_quant.plan import embed_weight_image
     rng = np.random.default_rng(n * 1000 + N)
     q = rng.integers(-128, 128, size=(n, 3, h, w), dtype=np.int8)
     s = np.float32(0.0173)
@@ -163,7 +168,8 @@ def test_embed_q_equals_patchify_then_sgemm_embed(n, h, w, N, zp):
     _lib.call("nqk_patchify_dequant", qd.vp, cols.vp, n, 3, h, w, 16, 16, float(s), zp)
     ref = DeviceArray((n, hw + 1, N), np.float32)
     _lib.call("nqk_sgemm_embed", cols.vp, wm.vp, bias.vp, cls.vp, pos.vp, ref.vp, n, hw, N, 768)
-    wt = permute(permute(Wd, [0, 2, 3, 1]).reshape((N, 48, 8, 2)), [0, 1, 3, 2]).reshape((N, 768))
+    assert _lib.load().nqk_embed_weight_order() == int(mfma)
+    wt = embed_weight_image(Wd, N, 768)
     out = DeviceArray((n, hw + 1, N), np.float32)
     _lib.call("nqk_embed_q", qd.vp, float(s), zp, wt.vp, bias.vp, cls.vp, pos.vp, out.vp, n, 3, h, w, 16, 16, N)
     np.testing.assert_array_equal(out.to_host().view(np.int32), ref.to_host().view(np.int32))

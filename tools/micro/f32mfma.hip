@@ -54,12 +54,18 @@ __global__ void __launch_bounds__(512, 1) k_rate(int iters, float* out, long lon
       for (int q = 0; q < 16; ++q) acc[q & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[q & 3], 0, 0, 0);
     for (int i = 0; i < 4; ++i) s += acc[i][0];
   } else {
+    // SHAPE 32: four independent accumulator chains in rotation; 322: two (round 6: the order the
+    // compiler gives k_embed_q's loop); 321: one
+    constexpr int CH = SHAPE == 32 ? 4 : (SHAPE == 322 ? 2 : 1);
     v16f acc[4];
     for (int i = 0; i < 4; ++i)
       for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
     for (int it = 0; it < iters; ++it)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q & 3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[q & 3], 0, 0, 0);
+      for (int q = 0; q < 4; ++q) {
+        acc[q % CH] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[q % CH], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     for (int i = 0; i < 4; ++i) s += acc[i][0];
   }
   long long t1 = __builtin_amdgcn_s_memtime();
@@ -105,12 +111,14 @@ int main() {
   float* out; long long* clk;
   hipMalloc(&out, 4); hipMalloc(&clk, cus * 8);
   const int iters = 20000;
-  for (int shape : {16, 32}) {
+  for (int shape : {16, 32, 322, 321}) {
     for (int rep = 0; rep < 2; ++rep) {
       hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
       hipEventRecord(e0);
       if (shape == 16) hipLaunchKernelGGL(k_rate<16>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
-      else hipLaunchKernelGGL(k_rate<32>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
+      else if (shape == 32) hipLaunchKernelGGL(k_rate<32>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
+      else if (shape == 322) hipLaunchKernelGGL(k_rate<322>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
+      else hipLaunchKernelGGL(k_rate<321>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
       hipEventRecord(e1); hipEventSynchronize(e1);
       float ms; hipEventElapsedTime(&ms, e0, e1);
       // flops per wave: 16x16x4: 16 instr x 2048 flops per iter; 32x32x2: 4 x 4096
