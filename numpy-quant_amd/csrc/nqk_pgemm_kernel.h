@@ -93,6 +93,11 @@ constexpr int pg_lds_bytes(int epi, bool b4, int wm = 1, int nk = 12) {
 #ifndef NQK_PG_RESQ
 #define NQK_PG_RESQ 3  // the residual epilogue's subtiles of residual rows in flight (round 6 A/B: 4)
 #endif
+#ifndef NQK_PG_RDIRECT
+#define NQK_PG_RDIRECT 0  // 1: the residual epilogue straight from the accumulator layout (no LDS transposes),
+                          // so ring slot 2 is free and all three stages of the next tile go out before the
+                          // epilogue's stores (round 6 A/B)
+#endif
 #ifndef NQK_PG_SPREAD
 #define NQK_PG_SPREAD 0  // 1: the stage's LDS-DMA pieces spread over the first half step (A/B variant)
 #endif
@@ -814,16 +819,62 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   int8_t* const tr = lds + (B4 || WM == 2 ? COLP + 4096 : 2 * STG) + wave * (16 * TR_ROW);
   const int ta = lane & 15, tb = lane >> 4;
   constexpr int RQ = NQK_PG_RESQ;  // residual subtiles in flight (register slots)
+  // DIRECT (NQK_PG_RDIRECT): no transposes, ring slot 2 stays free, PRE = the last stage of the next
+  // tile issued before this tile's epilogue (RD - 2 otherwise)
+  constexpr bool DIRECT = RESID && NQK_PG_RDIRECT && !B4 && WM == 1 && !RB;
+  constexpr int PRE = DIRECT ? RD - 1 : RD - 2;
   v4u resv[RQ][4];
   auto res_off = [&](const Src& s, int i, int k) __attribute__((always_inline)) {
     return (uint32_t)(((s.r0 + PG_BM * wm + 16 * i + 4 * k + tb) * e.ldo + s.tn * PG_BN + 64 * wn + 4 * ta) * 4);
+  };
+  // DIRECT: lane (l15, lg) of subtile i, column block j: row 16 i + l15, columns 16 j + 4 lg .. + 3 of
+  // the wave's 64 — the accumulator layout itself (16 rows x 64 B per instruction)
+  auto res_off_d = [&](const Src& s, int i, int j) __attribute__((always_inline)) {
+    return (uint32_t)(((s.r0 + PG_BM * wm + 16 * i + l15) * e.ldo + s.tn * PG_BN + 64 * wn + 16 * j + 4 * lg) * 4);
   };
   auto res_issue = [&](const Src& s, auto I) __attribute__((always_inline)) {
     constexpr int i = decltype(I)::value;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      resv[i % RQ][k] = pg_load16(s.tn * PG_BN + 64 * wn < N && (NQK_PG_DIAG & 4096) == 0 ? r_res : r_nul, res_off(s, i, k), 0u,
+      resv[i % RQ][k] = pg_load16(s.tn * PG_BN + 64 * wn < N && (NQK_PG_DIAG & 4096) == 0 ? r_res : r_nul,
+                                 DIRECT ? res_off_d(s, i, k) : res_off(s, i, k), 0u,
                                  NQK_PG_RLAUX >= 0 ? NQK_PG_RLAUX : (NK == 48 ? 2 : 0));
+  };
+  auto epilogue_resid_direct = [&](const Src& s, int cslot) __attribute__((always_inline)) {
+    const int8_t* cp = lds + COLP + cslot * 2048;
+    v4i bj[4];  // bias of columns 16 j + 4 lg .. + 3
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bj[j] = pg_lds16(cp + 1024 + (64 * wn + 16 * j + 4 * lg) * 4);
+    const rsrc_t r_out = pg_rsrc(e.out[0], s.tn * PG_BN + 64 * wn < N ? (uint32_t)((uint64_t)M * e.ldo * 4) : 0u);
+    const float sacc = e.sacc[0];
+    sfor<0, 8>([&](auto I) __attribute__((always_inline)) {
+      constexpr int i = decltype(I)::value;
+      const v4u(&rv)[4] = resv[i % RQ];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const v4i t = acc[i][j];
+        const v4i bb = bj[j];
+        v4u st;
+        if constexpr (F32X) {
+          const v2f b01 = v2f{__int_as_float(bb[0]), __int_as_float(bb[1])};
+          const v2f b23 = v2f{__int_as_float(bb[2]), __int_as_float(bb[3])};
+          const v2f d01 = v2f{(float)t[0], (float)t[1]} * v2f{sacc, sacc};
+          const v2f d23 = v2f{(float)t[2], (float)t[3]} * v2f{sacc, sacc};
+          const v2f y01 = (b01 + d01) + v2f{__uint_as_float(rv[j][0]), __uint_as_float(rv[j][1])};
+          const v2f y23 = (b23 + d23) + v2f{__uint_as_float(rv[j][2]), __uint_as_float(rv[j][3])};
+          st = v4u{__float_as_uint(y01[0]), __float_as_uint(y01[1]), __float_as_uint(y23[0]), __float_as_uint(y23[1])};
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = (float)((double)t[r] * (double)sacc);
+            st[r] = __float_as_uint((__int_as_float(bb[r]) + d) + __uint_as_float(rv[j][r]));
+          }
+        }
+        if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
+        else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, res_off_d(s, i, j), 0, NQK_PG_STAUX_RESID);
+      }
+      if constexpr (i + RQ - 1 < 8) res_issue(s, ic<i + RQ - 1>{});
+    });
   };
   auto epilogue_resid = [&](const Src& s, int cslot) __attribute__((always_inline)) {
     const int8_t* cp = lds + COLP + cslot * 2048;
@@ -955,7 +1006,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
   // read zeros, so a caller's buffer of exactly the table's size is never over-read)
   if constexpr (pg_is_glut(EPI)) pg_dma16(pg_rsrc(e.lut, e.lut_bytes), lds + LUTO + wave * 1024, 16 * lane, 1024u * wave);
   issue_colp(cur.tn, 0);
-  sfor<0, RD - 1>([&](auto S) __attribute__((always_inline)) { issue_stage(cur, decltype(S)::value, decltype(S)::value); });
+  sfor<0, PRE + 1>([&](auto S) __attribute__((always_inline)) { issue_stage(cur, decltype(S)::value, decltype(S)::value); });
   if constexpr (NQK_PG_PRIO == 2) {
     if ((int)blockIdx.x >= G / 2) __builtin_amdgcn_s_setprio(1);
   }
@@ -967,8 +1018,8 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     const int cs = it & 1;
     // stage 0 and this tile's column constants landed (younger: stages 1 .. RD - 2, the previous
     // epilogue's operations)
-    if (it == 0) pg_vmcnt<(RD - 2) * PWA>();
-    else pg_vmcnt<(RD - 2) * PWA + EOPS>();
+    if (it == 0) pg_vmcnt<PRE * PWA>();
+    else pg_vmcnt<PRE * PWA + EOPS>();
     if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     // initial accumulators: minus the zero-point column terms of the lane's 16 columns
@@ -1005,13 +1056,13 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         v4i(&an)[4] = (kt & 1) ? a_lo : a_hi;
         if constexpr (kt > 0) pg_lgkm_tie8(ac, bc);
         quarter(ic<0>{}, std::integral_constant<bool, kt == 0>{}, ac, bc, cinit, [&](auto Q) __attribute__((always_inline)) {
-          if constexpr (kt + RD - 1 < NK && decltype(Q)::value == 4) issue_stage(cur, kt + RD - 1, (kt + RD - 1) % RD);
+          if constexpr (kt + RD - 1 < NK && kt + RD - 1 > PRE && decltype(Q)::value == 4) issue_stage(cur, kt + RD - 1, (kt + RD - 1) % RD);
         });
         if constexpr (kt == 1) issue_colp(nxt.tn, cs ^ 1);
         if constexpr (kt + 1 < NK) {
           constexpr int hi_s = (kt + RD - 1 < NK ? kt + RD - 1 : NK - 1);
           constexpr int y = (hi_s >= kt + 2 ? (hi_s - kt - 1) * PWA : 0) + ((kt >= 1 && kt <= RD - 1) ? 1 : 0);
-          if (kt + 1 <= RD - 2 && it > 0) pg_vmcnt<y + EOPS>();
+          if (kt + 1 <= PRE && it > 0) pg_vmcnt<y + EOPS>();
           else pg_vmcnt<y>();
           if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
@@ -1041,7 +1092,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         // stage kt + 2: NQK_PG_SPREAD 0 = all pieces after MFMA 4; 1 = one piece every
         // other MFMA from MFMA 1 (a burst of LDS-DMA issues costs each piece more:
         // MI355X_MICROARCH.md, LDS-DMA piece issue cost)
-        if constexpr (kt + RD - 1 < NK) {
+        if constexpr (kt + RD - 1 < NK && kt + RD - 1 > PRE) {
           if constexpr (NQK_PG_SPREAD == 0) {
             if constexpr (q == 4) issue_stage(cur, kt + RD - 1, (kt + RD - 1) % RD);
           } else if constexpr ((q & 1) == 1 && (q >> 1) < PW) {
@@ -1056,7 +1107,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
         // previous tile's epilogue operations
         constexpr int hi_s = (kt + RD - 1 < NK ? kt + RD - 1 : NK - 1);
         constexpr int y = (hi_s >= kt + 2 ? (hi_s - kt - 1) * PWA : 0) + ((kt >= 1 && kt <= RD - 1) ? 1 : 0);
-        if (kt + 1 <= RD - 2 && it > 0) pg_vmcnt<y + EOPS>();
+        if (kt + 1 <= PRE && it > 0) pg_vmcnt<y + EOPS>();
         else pg_vmcnt<y>();
         pg_lgkm_tie(a_hi[0], a_hi[1], a_hi[2], a_hi[3]);
         if constexpr ((NQK_PG_DIAG & 8) == 0) __builtin_amdgcn_s_barrier();
@@ -1084,7 +1135,7 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
     }
     // (the last tile re-stages its own first stages: never read, drained at the end; the
     // VMEM counts stay the same on every path)
-    sfor<0, RD - 1>([&](auto S) __attribute__((always_inline)) { issue_stage(nxt, decltype(S)::value, decltype(S)::value); });
+    sfor<0, PRE + 1>([&](auto S) __attribute__((always_inline)) { issue_stage(nxt, decltype(S)::value, decltype(S)::value); });
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (NQK_PG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     if constexpr (NQK_PG_PRIO == 3) __builtin_amdgcn_s_setprio(1);
@@ -1094,7 +1145,8 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = acc[i][j] >> 4;
     }
-    if constexpr (RESID) epilogue_resid(cur, cs);
+    if constexpr (DIRECT) epilogue_resid_direct(cur, cs);
+    else if constexpr (RESID) epilogue_resid(cur, cs);
     else epilogue(cur, cs);
     cur = nxt;
   }

@@ -158,6 +158,21 @@ for name in sel:
             except RuntimeError as ex:
                 print(vname, ex, flush=True)
                 res[vname].append(float("nan"))
+    if os.environ.get("PGM_CHECK") and epi == 3:  # every build's residual output against the main build's
+        out_arr, ref = keep[8], None
+        for vname, lib, env, use_pg in variants:
+            if use_pg is not True:
+                continue
+            e.bt_pg = pg.ptr
+            out_arr.fill_zero()
+            sync_all()
+            args = (epi, a.vp, bt.vp, 1, M, N, K, K, K, None, 0, 0, ctypes.byref(e))
+            assert lib.nqk_qgemm_fused(*args) == 0
+            sync_all()
+            h = out_arr.to_host()
+            ref = h if ref is None else ref
+            ok = np.array_equal(h.view(np.int32), ref.view(np.int32))
+            print(f"check {name} {vname}: {'equal' if ok else 'DIFF %d' % int((h != ref).sum())}", flush=True)
     for vname, ts in res.items():
         t = min(ts)
         print(f"{name:5s} {vname:14s} M={M} N={N} K={K}: min {t:7.1f} us  med {sorted(ts)[len(ts) // 2]:7.1f} us  "
