@@ -688,6 +688,10 @@ k_pg(const int8_t* __restrict__ A, const int8_t* __restrict__ Bp, int M, int N, 
             }
           }
           const v4u st = v4u{pk[0], pk[1], pk[2], pk[3]};
+          // (diagnostic 8192, wrong layout: the wave's 16 rows x 64 B of a subtile as 1 KiB contiguous
+          // — whole lines per instruction, the same bytes per launch: does the half-line row pattern cost?)
+          if constexpr ((NQK_PG_DIAG & 8192) != 0)
+            off = (uint32_t)((s.r0 + PG_BM * wm + 16 * i) * e.ldo + (s.tn * 4 + wn) * 1024 + 16 * lane);
           if constexpr ((NQK_PG_DIAG & 1) != 0) asm volatile("" ::"v"(st[0] ^ st[1] ^ st[2] ^ st[3]));
           else __builtin_amdgcn_raw_buffer_store_b128(st, r_out, off, 0, NQK_PG_STAUX);
           return;
