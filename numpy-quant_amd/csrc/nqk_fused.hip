@@ -582,6 +582,9 @@ constexpr int PP_LDS = (NQK_PP_PD + 1) * (256 + GBN) * GBK;  // 96 KiB at depth 
 #ifndef NQK_DIAG
 #define NQK_DIAG 0
 #endif
+#ifndef NQK_BIG_RPRE
+#define NQK_BIG_RPRE 0  // 1: k_qgemm_big<RESID> issues pass 0's residual rows before the k loop (round 6 A/B: no gain)
+#endif
 #ifndef NQK_GLDS_FIRST
 #define NQK_GLDS_FIRST 0  // diagnostic builds: issue the next stage's LDS-DMA before the reads
 #endif
@@ -611,9 +614,20 @@ template <int CTRL>  // v of another lane of the 16-lane row (DPP: no LDS round 
 __device__ __forceinline__ float ln_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
-template <int EPI, bool I32, bool F32X, int ASH = 0, bool LN = false>
+// the residual rows of pass `pass` of a 128-row tile (rows mw + 32 pass + 4 it + (lane >> 4), the
+// lane's 4 columns gn0 ..): proj_epilogue's loads, also issued by k_qgemm_big before its k loop
+__device__ __forceinline__ void proj_res_load(const Epi& e, int mw, int gn0, bool cok, int M, int N, int lane, int pass,
+                                              float4 (&dst)[G_RP / 4]) {
+#pragma unroll
+  for (int it = 0; it < G_RP / 4; ++it) {
+    const int gm = min(mw + pass * G_RP + it * 4 + (lane >> 4), M - 1);
+    dst[it] = cok ? *reinterpret_cast<const float4*>(e.resid + (int64_t)gm * N + gn0) : make_float4(0, 0, 0, 0);
+  }
+}
+// PRE0 (round 6): pass 0's residual rows were loaded by the caller before its k loop (rv0)
+template <int EPI, bool I32, bool F32X, int ASH = 0, bool LN = false, bool PRE0 = false>
 __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], const Epi& e, int mw, int ncol0,
-                                              int M, int N, int wave, int lane) {
+                                              int M, int N, int wave, int lane, const float4 (*rv0)[G_RP / 4] = nullptr) {
   constexpr int RP = G_RP;
   static_assert(!LN || EPI == EPI_RESID, "proj_epilogue: the LayerNorm fuses into the residual epilogue");
   const int r32 = lane & 31, half = lane >> 5;
@@ -639,14 +653,15 @@ __device__ __forceinline__ void proj_epilogue(int8_t* lds, v16i (&acc)[4][2], co
   // issued right after the previous pass is staged (two register sets; the staged
   // accumulators of earlier passes are dead by then)
   float4 rv[2][RP / 4];
-  auto load_res = [&](int pass, float4 (&dst)[RP / 4]) {
+  auto load_res = [&](int pass, float4 (&dst)[RP / 4]) { proj_res_load(e, mw, gn0, cok, M, N, lane, pass, dst); };
+  if constexpr (EPI == EPI_RESID) {
+    if constexpr (PRE0) {
 #pragma unroll
-    for (int it = 0; it < RP / 4; ++it) {
-      const int gm = min(mw + pass * RP + it * 4 + (lane >> 4), M - 1);
-      dst[it] = cok ? *reinterpret_cast<const float4*>(e.resid + (int64_t)gm * N + gn0) : make_float4(0, 0, 0, 0);
+      for (int it = 0; it < RP / 4; ++it) rv[0][it] = (*rv0)[it];
+    } else {
+      load_res(0, rv[0]);
     }
-  };
-  if constexpr (EPI == EPI_RESID) load_res(0, rv[0]);
+  }
 #pragma unroll
   for (int pass = 0; pass < 128 / RP; ++pass) {
 #pragma unroll
@@ -977,6 +992,16 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   using S1 = std::integral_constant<int, 1>;
   using S2 = std::integral_constant<int, 2>;
   const int nk = K / GBK;  // a multiple of 3 (host-checked): the ring slot of step kt is kt % 3
+  // RESID (NQK_BIG_RPRE=1, opt-in; round 6, no gain: profiles/r06_big_rpre_dropped.txt): pass 0's residual rows issued before the k loop, so
+  // the epilogue does not open on their HBM latency (ViT-Ti's residual GEMMs: 2 workgroups per CU
+  // at most, latency-bound); the vmcnt waits of the loop count LDS-DMA operations only, so these
+  // older loads are waited for with the first stage (vmcnt is in order)
+  constexpr bool RPRE = EPI == EPI_RESID && NQK_BIG_RPRE;
+  float4 rv0[G_RP / 4];
+  if constexpr (RPRE) {
+    const int gn0 = n0 + wn * 64 + (lane & 15) * 4;
+    proj_res_load(e, m0, gn0, gn0 < N, M, N, lane, 0, rv0);
+  }
   issue(0, S0{});
   issue(1, S1{});
   for (int kt = 0; kt + 3 < nk; kt += 3) {  // every step refills (stage kt + 4 < nk)
@@ -989,7 +1014,8 @@ k_qgemm_big(const int8_t* __restrict__ A, const int8_t* __restrict__ Bt, int M, 
   kstep(nk - 1, S2{}, F_{}, T_{});
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  proj_epilogue<EPI, I32, F32X, B4 ? 4 : 0, LN>(lds, acc, e, m0, n0 + wn * 64, M, N, wave, lane);
+  if constexpr (RPRE) proj_epilogue<EPI, I32, F32X, B4 ? 4 : 0, LN, true>(lds, acc, e, m0, n0 + wn * 64, M, N, wave, lane, &rv0);
+  else proj_epilogue<EPI, I32, F32X, B4 ? 4 : 0, LN>(lds, acc, e, m0, n0 + wn * 64, M, N, wave, lane);
 }
 
 template <int EPI, bool I32, bool F32X>
