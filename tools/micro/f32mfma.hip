@@ -44,6 +44,12 @@ template <int SHAPE>
 __global__ void __launch_bounds__(512, 1) k_rate(int iters, float* out, long long* clk) {
   const int lane = threadIdx.x & 63;
   float a = 1.0f + lane * 1e-3f, b = 0.5f - lane * 1e-3f;
+  if constexpr (SHAPE >= 1000) {  // (round 6) random-looking operands: a hash of (lane, block), sign and exponent spread
+    uint32_t h = (uint32_t)(threadIdx.x * 2654435761u) ^ (uint32_t)(blockIdx.x * 40503u);
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    a = __uint_as_float((h & 0x807fffffu) | 0x3f000000u);          // +-[0.5, 1)
+    b = __uint_as_float(((h * 2246822519u) & 0x807fffffu) | 0x3e800000u);  // +-[0.25, 0.5)
+  }
   long long t0 = __builtin_amdgcn_s_memtime();
   float s = 0.0f;
   if constexpr (SHAPE == 16) {
@@ -55,15 +61,18 @@ __global__ void __launch_bounds__(512, 1) k_rate(int iters, float* out, long lon
     for (int i = 0; i < 4; ++i) s += acc[i][0];
   } else {
     // SHAPE 32: four independent accumulator chains in rotation; 322: two (round 6: the order the
-    // compiler gives k_embed_q's loop); 321: one
-    constexpr int CH = SHAPE == 32 ? 4 : (SHAPE == 322 ? 2 : 1);
+    // compiler gives k_embed_q's loop); 321: one; 1032: four, random-looking operands whose bits
+    // change every instruction (a, b rotated through 4 values per lane)
+    constexpr int CH = (SHAPE == 32 || SHAPE == 1032) ? 4 : (SHAPE == 322 ? 2 : 1);
     v16f acc[4];
     for (int i = 0; i < 4; ++i)
       for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+    float av[4] = {a, -b, b * 1.75f, -a * 0.625f}, bv[4] = {b, a * 0.875f, -a, b * 1.5f};
     for (int it = 0; it < iters; ++it)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        acc[q % CH] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[q % CH], 0, 0, 0);
+        const float aa = SHAPE == 1032 ? av[q] : a, bb = SHAPE == 1032 ? bv[(q + 1) & 3] : b;
+        acc[q % CH] = __builtin_amdgcn_mfma_f32_32x32x2f32(aa, bb, acc[q % CH], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
     for (int i = 0; i < 4; ++i) s += acc[i][0];
@@ -111,18 +120,19 @@ int main() {
   float* out; long long* clk;
   hipMalloc(&out, 4); hipMalloc(&clk, cus * 8);
   const int iters = 20000;
-  for (int shape : {16, 32, 322, 321}) {
+  for (int shape : {16, 32, 322, 321, 1032}) {
     for (int rep = 0; rep < 2; ++rep) {
       hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
       hipEventRecord(e0);
       if (shape == 16) hipLaunchKernelGGL(k_rate<16>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
       else if (shape == 32) hipLaunchKernelGGL(k_rate<32>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
       else if (shape == 322) hipLaunchKernelGGL(k_rate<322>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
+      else if (shape == 1032) hipLaunchKernelGGL(k_rate<1032>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
       else hipLaunchKernelGGL(k_rate<321>, dim3(cus), dim3(512), 0, 0, iters, out, clk);
       hipEventRecord(e1); hipEventSynchronize(e1);
       float ms; hipEventElapsedTime(&ms, e0, e1);
       // flops per wave: 16x16x4: 16 instr x 2048 flops per iter; 32x32x2: 4 x 4096
-      const double flops = (double)cus * 8 * iters * (shape == 16 ? 16 * 2048.0 : 4 * 4096.0);
+      const double flops = (double)cus * 8 * iters * (shape == 16 ? 16 * 2048.0 : 4 * 4096.0);  // (1032: as 32)
       long long c0; hipMemcpy(&c0, clk, 8, hipMemcpyDeviceToHost);
       printf("rate %dx%d f32: %.3f ms  %.1f TFLOP/s  (shader clock ~%.2f GHz from s_memtime)\n", shape, shape, ms,
              flops / ms / 1e9, c0 / (ms * 1e6));
